@@ -1,0 +1,94 @@
+"""Device-resident batches of independent jobs (layer 1 of include/efes_hash.h).
+
+A batch is N independent `Write(p)` (+ Sum) jobs over messages that already live in
+device memory -- the shape of many concurrent uploads (filereceiver.go:208-209, one
+request goroutine per upload).  Device buffers are torch tensors (plumbing only); the
+hashing is libefeshash.so.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from ._lib import EFES_JOB_FINALIZE, JOB_DTYPE, MODE_AUTO, SHA1_STATE_DTYPE
+from .hashing import Context, default_context
+
+IV = np.array([0x67452301, 0xEFCDAB89, 0x98BADCFE, 0x10325476, 0xC3D2E1F0], dtype=np.uint32)
+
+
+def fresh_states(n: int) -> np.ndarray:
+    """n states equal to NewSha1() (sha1.go:48-52)."""
+    st = np.zeros(n, dtype=SHA1_STATE_DTYPE)
+    st["h"][:] = IV
+    return st
+
+
+class DeviceBatch:
+    """Jobs j = 0..N-1: Write(data[offsets[j] : offsets[j]+lengths[j]]) into state j (+ Sum)."""
+
+    def __init__(self, data_ptr: int, offsets, lengths, *, sha1: bool = True, crc32: bool = True,
+                 finalize: bool = True, states: np.ndarray | None = None, crcs: np.ndarray | None = None,
+                 ctx: Context | None = None, device: str = "cuda:0"):
+        import torch
+
+        self.ctx = ctx or default_context(int(device.split(":")[1]) if ":" in device else 0)
+        self.torch = torch
+        self.device = device
+        offsets = np.asarray(offsets, dtype=np.uint64)
+        lengths = np.asarray(lengths, dtype=np.uint64)
+        n = self.n = int(offsets.size)
+        assert lengths.size == n
+        self.init_states = fresh_states(n) if states is None else np.array(states, dtype=SHA1_STATE_DTYPE)
+        self.init_crcs = np.zeros(n, np.uint32) if crcs is None else np.asarray(crcs, dtype=np.uint32)
+        self._init_states_dev = torch.from_numpy(self.init_states.view(np.uint8).copy()).to(device)
+        self._init_crcs_dev = torch.from_numpy(self.init_crcs.view(np.uint8).copy()).to(device)
+        self.states = self._init_states_dev.clone()
+        self.crcs = self._init_crcs_dev.clone()
+        self.sums = torch.zeros(max(n, 1) * 24, dtype=torch.uint8, device=device)
+        self.status = torch.full((max(n, 1),), -99, dtype=torch.int32, device=device)
+        jobs = np.zeros(n, dtype=JOB_DTYPE)
+        jobs["data"] = np.uint64(data_ptr) + offsets
+        jobs["length"] = lengths
+        if sha1:
+            jobs["sha1"] = np.uint64(self.states.data_ptr()) + np.arange(n, dtype=np.uint64) * np.uint64(104)
+        if crc32:
+            jobs["crc32"] = np.uint64(self.crcs.data_ptr()) + np.arange(n, dtype=np.uint64) * np.uint64(4)
+        if finalize:
+            jobs["sum"] = np.uint64(self.sums.data_ptr()) + np.arange(n, dtype=np.uint64) * np.uint64(24)
+            jobs["flags"] = EFES_JOB_FINALIZE
+        jobs["status"] = np.uint64(self.status.data_ptr()) + np.arange(n, dtype=np.uint64) * np.uint64(4)
+        self.jobs_host = jobs
+        self.jobs = torch.from_numpy(jobs.view(np.uint8).copy()).to(device)
+        torch.cuda.synchronize(device)
+
+    def stream(self) -> int:
+        return self.torch.cuda.current_stream(self.device).cuda_stream
+
+    def reset(self) -> None:
+        """Restore the initial states (async, on torch's current stream)."""
+        self.states.copy_(self._init_states_dev)
+        self.crcs.copy_(self._init_crcs_dev)
+
+    def submit(self, mode: int = MODE_AUTO) -> None:
+        """Enqueue all jobs on torch's current stream (ordered after the data it wrote)."""
+        self.ctx.submit(self.jobs.data_ptr(), self.n, self.stream(), mode)
+
+    def run(self, mode: int = MODE_AUTO) -> None:
+        self.submit(mode)
+        self.torch.cuda.synchronize(self.device)
+
+    # ---- results (host copies)
+    def status_host(self) -> np.ndarray:
+        return self.status.cpu().numpy()[: self.n]
+
+    def sums_host(self) -> np.ndarray:
+        return self.sums.cpu().numpy()[: self.n * 24].reshape(self.n, 24)
+
+    def sha1_hex(self) -> list[str]:
+        s = self.sums_host()
+        return [bytes(r[:20]).hex() for r in s]
+
+    def crc_sum(self) -> np.ndarray:
+        return self.crcs.cpu().numpy().view(np.uint32)[: self.n]
+
+    def states_host(self) -> np.ndarray:
+        return self.states.cpu().numpy().view(SHA1_STATE_DTYPE)[: self.n]

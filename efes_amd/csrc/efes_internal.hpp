@@ -1,0 +1,32 @@
+// efes_internal.hpp -- shared between the kernels (efes_kernels.hip) and the C ABI (efes_api.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/efes_hash.h"
+
+namespace efes {
+
+// CRC-32/IEEE tables resident in HBM, copied into LDS by every workgroup.
+//   slice8: the slicing-by-8 table of crc32.go:138-149 (slice8[0] == IEEETable).
+//   shift[k][b][v]: the raw (un-inverted, reflected) CRC register v<<(8b) advanced over
+//   (64 << k) zero bytes, i.e. multiplication by x^(8*64*2^k) mod P.  The register map
+//   is GF(2)-linear, so advancing any register is the XOR of its four byte lookups.
+//   Used to combine per-block CRCs (crc(A||B) = shift(crc(A), |B|) ^ crc(B)).
+constexpr int kShiftLevels = 7;  // 64 B .. 4 KiB
+struct Tables {
+  uint32_t slice8[8][256];
+  uint32_t shift[kShiftLevels][4][256];
+};
+
+void build_tables(Tables* t);  // host
+
+// Launchers (host side, defined in efes_kernels.hip).
+hipError_t launch_deep(const efes_job* jobs, uint32_t njobs, const Tables* tabs, hipStream_t s);
+hipError_t launch_wide(const efes_job* jobs, uint32_t njobs, const Tables* tabs, hipStream_t s);
+hipError_t launch_fill(void* dst, size_t bytes, uint64_t seed, hipStream_t s);
+
+constexpr int kDeepWaves = 4;  // waves per DEEP workgroup: one per SIMD
+constexpr uint32_t kAutoDeepMaxJobs = 1536;  // AUTO: DEEP up to ~1.5 waves per SIMD
+
+}  // namespace efes

@@ -1,0 +1,540 @@
+// efes_kernels.hip -- MI355X (gfx950) kernels for efes' per-chunk SHA-1 + CRC-32/IEEE.
+//
+// Semantics: every efes_job is one `Write(p)` of the reference's
+//   sha1digest.Write  (/root/reference/sha1.go:58-79)  and
+//   crc32digest.Write (/root/reference/crc32.go:76-86 -> slicingUpdate :153-169)
+// into a device-resident state, optionally followed by Sum (sha1.go:82-120 checkSum,
+// crc32.go:88-93).  Go panics (nx > 64 at Write, d.nx != 0 in checkSum) become
+// EFES_ERR_STATE.  The tail buffer x is updated byte-for-byte as Go does, stale bytes
+// included, so MarshalText (sha1_efes.go:25-38) of a device state equals Go's.
+//
+// Two kernel shapes:
+//   DEEP: one wavefront per job.  SHA-1 is a strict chain of 64-byte compressions, so a
+//         job's speed is one wave's issue rate.  The 64 lanes load 64 consecutive blocks
+//         (4 KiB, coalesced), compute their CRC-32 partials and expand their message
+//         schedules W[i]+K[i] into LDS in parallel; the per-block CRCs are combined by a
+//         6-level GF(2) shift tree; then the wave runs the 80-round chain reading WK from
+//         LDS: 5 VALU + 1/4 ds_read_b128 per round, the minimum we found.
+//   WIDE: one lane per job (64 jobs per wave), schedule inline, CRC fused per lane.
+//         Throughput shape for many concurrent jobs.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include "efes_internal.hpp"
+#include "sha1_device.hpp"
+
+namespace efes {
+
+// ------------------------------------------------------------------ CRC-32 helpers
+// Raw (register-level) reflected CRC: Go's update is ~raw(~crc, p) (crc32.go:123,127,155,165).
+__device__ __forceinline__ uint32_t crc_byte(const uint32_t* __restrict__ t0, uint32_t crc, uint32_t b) {
+  return t0[(crc ^ b) & 0xffu] ^ (crc >> 8);  // crc32.go:125
+}
+
+__device__ __forceinline__ uint32_t crc_shift(const uint32_t (&s)[4][256], uint32_t v) {
+  return s[0][v & 0xffu] ^ s[1][(v >> 8) & 0xffu] ^ s[2][(v >> 16) & 0xffu] ^ s[3][v >> 24];
+}
+
+// Slicing-by-8 over 64 bytes held as 16 little-endian words (crc32.go:157-161).
+__device__ __forceinline__ uint32_t crc_words_raw(const uint32_t (&t)[8][256], uint32_t crc, const uint32_t (&le)[16]) {
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    const uint32_t hi = le[2 * s + 1];
+    crc ^= le[2 * s];
+    crc = t[0][hi >> 24] ^ t[1][(hi >> 16) & 0xffu] ^ t[2][(hi >> 8) & 0xffu] ^ t[3][hi & 0xffu] ^
+          t[4][crc >> 24] ^ t[5][(crc >> 16) & 0xffu] ^ t[6][(crc >> 8) & 0xffu] ^ t[7][crc & 0xffu];
+  }
+  return crc;
+}
+
+__device__ __forceinline__ uint32_t uniform32(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t uniform64(uint64_t v) {
+  return (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)v) |
+         ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32);
+}
+
+// Orders this wave's LDS stores before its later LDS loads from other lanes.
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Big-endian word k (bytes 4k..4k+3) of a byte array in LDS.
+__device__ __forceinline__ uint32_t be_word_lds(const uint8_t* b, int k) {
+  return (uint32_t)b[4 * k] << 24 | (uint32_t)b[4 * k + 1] << 16 | (uint32_t)b[4 * k + 2] << 8 | b[4 * k + 3];
+}
+
+// Load 64 bytes at an arbitrary device address as 16 little-endian words.
+// kAligned16: the address is 16-byte aligned (4 x global_load_dwordx4).
+// Otherwise: 16 (or 17) naturally aligned dword loads funnel-shifted by v_alignbyte.  The
+// 17th dword is loaded only when the block is misaligned, and then it holds a byte of the
+// block, so it never touches a page the block does not touch.
+template <bool kAligned16>
+__device__ __forceinline__ void load_block_le(const uint8_t* src, uint32_t (&le)[16]) {
+  if constexpr (kAligned16) {
+    const uint4* s = reinterpret_cast<const uint4*>(src);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint4 v = s[q];
+      le[4 * q] = v.x; le[4 * q + 1] = v.y; le[4 * q + 2] = v.z; le[4 * q + 3] = v.w;
+    }
+  } else {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(src);
+    const uint32_t* s = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(a & 3);
+    uint32_t d[17];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) d[k] = s[k];
+    d[16] = sh ? s[16] : 0u;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) le[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+  }
+}
+
+// ================================================================== DEEP kernel
+constexpr int kWKStride = 80;  // words per expanded block in LDS
+
+struct DeepLDS {
+  Tables tab;                                    // 36 KiB
+  uint32_t wk[kDeepWaves][64][kWKStride];        // 80 KiB: W[i]+K[i] of 64 blocks per wave
+  uint8_t xs[kDeepWaves][64];                    // the job's tail buffer x (sha1.go:31)
+  uint8_t fin[kDeepWaves][192];                  // padding assembly for checkSum
+};
+
+struct DeepJob {
+  const uint8_t* p;
+  uint64_t plen;
+  efes_sha1_state* st;
+  efes_crc32_state* cs;
+  uint8_t* sum;
+  int32_t* status;
+  uint32_t flags;
+};
+
+// Bulk blocks q[0 .. 64*nbulk): CRC partials + schedule expansion by the 64 lanes, chain by the wave.
+template <bool kAligned16>
+__device__ void deep_bulk(DeepLDS& L, int wave, int lane, const uint8_t* q, uint64_t nbulk, bool do_sha,
+                          bool do_crc, uint32_t (&h)[5], uint32_t& crc_raw) {
+  uint32_t (*wk)[kWKStride] = L.wk[wave];
+  uint32_t le[16];
+  // Super-step s covers blocks [64s, 64s+nb).  Blocks are right-aligned in the lanes
+  // (lane 64-nb+i holds block i) so that the zero CRCs of idle lanes lead the tree.
+  uint64_t b0 = 0;
+  int nb = (int)(nbulk < 64 ? nbulk : 64);
+  {
+    const int bi = lane - (64 - nb);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) le[k] = 0;
+    if (bi >= 0) load_block_le<kAligned16>(q + 64 * (uint64_t)bi, le);
+  }
+  while (b0 < nbulk) {
+    const int off = 64 - nb;
+    const int bi = lane - off;
+    if (do_crc) {
+      uint32_t r = crc_words_raw(L.tab.slice8, 0u, le);  // raw CRC of this lane's block, register 0
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {  // crc(A||B) = shift(crc(A), |B|) ^ crc(B), |B| = 64<<k bytes
+        const uint32_t o = __shfl_xor(r, 1 << k);
+        const bool right = (lane >> k) & 1;
+        r = crc_shift(L.tab.shift[k], right ? o : r) ^ (right ? r : o);
+      }
+      if (nb == 64) {
+        crc_raw = crc_shift(L.tab.shift[6], crc_raw);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 6; ++k)
+          if ((nb >> k) & 1) crc_raw = crc_shift(L.tab.shift[k], crc_raw);
+      }
+      crc_raw ^= r;
+    }
+    if (do_sha && bi >= 0) {
+      uint32_t w[16], x[80];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) w[k] = bswap(le[k]);
+      expand_wk(w, x);
+      uint4* dst = reinterpret_cast<uint4*>(wk[bi]);
+#pragma unroll
+      for (int k = 0; k < 20; ++k) dst[k] = make_uint4(x[4 * k], x[4 * k + 1], x[4 * k + 2], x[4 * k + 3]);
+    }
+    // Prefetch the next super-step's blocks; they land while the chain runs.
+    const uint64_t b1 = b0 + (uint64_t)nb;
+    const int nb1 = (int)((nbulk - b1) < 64 ? (nbulk - b1) : 64);
+    if (b1 < nbulk) {
+      const int bj = lane - (64 - nb1);
+#pragma unroll
+      for (int k = 0; k < 16; ++k) le[k] = 0;
+      if (bj >= 0) load_block_le<kAligned16>(q + 64 * (b1 + (uint64_t)bj), le);
+    }
+    if (do_sha) {
+      wave_lds_sync();
+      for (int j = 0; j < nb; ++j) compress_wk(h, reinterpret_cast<const uint4*>(wk[j]));
+      wave_lds_sync();
+    }
+    b0 = b1;
+    nb = nb1;
+  }
+}
+
+__device__ void deep_job(DeepLDS& L, int wave, int lane, const DeepJob& J) {
+  const bool do_sha = J.st != nullptr, do_crc = J.cs != nullptr;
+  const bool fin = (J.flags & EFES_JOB_FINALIZE) != 0;
+  uint8_t* xs = L.xs[wave];
+  int32_t status = EFES_OK;
+
+  uint32_t h[5] = {0, 0, 0, 0, 0};
+  int64_t nx = 0;
+  uint64_t len = 0;
+  if (do_sha) {
+#pragma unroll
+    for (int k = 0; k < 5; ++k) h[k] = uniform32(J.st->h[k]);
+    nx = (int64_t)uniform64((uint64_t)J.st->nx);
+    len = uniform64(J.st->len);
+    if (lane < 16) reinterpret_cast<uint32_t*>(xs)[lane] = reinterpret_cast<const uint32_t*>(J.st->x)[lane];
+  }
+  uint32_t crc_raw = do_crc ? ~uniform32(J.cs->crc) : 0u;
+
+  if (do_sha && nx > 64) {  // Go: copy(d.x[d.nx:], p) panics (sha1.go:62)
+    if (lane == 0 && J.status) *J.status = EFES_ERR_STATE;
+    return;
+  }
+  const uint8_t* p = J.p;
+  const uint64_t plen = J.plen;
+  wave_lds_sync();
+
+  // ---- head: complete the pending block x[:nx] (sha1.go:61-69)
+  uint64_t pos = 0;
+  int64_t nx_new = nx;
+  if (do_sha && nx > 0) {
+    const uint32_t room = (uint32_t)(64 - nx);
+    const uint32_t nh = plen < room ? (uint32_t)plen : room;
+    if ((uint32_t)lane < nh) xs[nx + lane] = p[lane];
+    wave_lds_sync();
+    if ((uint32_t)nx + nh == 64) {
+      uint32_t w[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) w[k] = be_word_lds(xs, k);
+      compress_inline(h, w);
+      nx_new = 0;
+    } else {
+      nx_new = nx + nh;
+    }
+    pos = nh;
+  }
+  if (do_crc)
+    for (uint64_t i = 0; i < pos; ++i) crc_raw = crc_byte(L.tab.slice8[0], crc_raw, p[i]);
+
+  // ---- bulk whole blocks (sha1.go:70-74)
+  const uint8_t* q = p + pos;
+  const uint64_t nbulk = (plen - pos) >> 6;
+  if (nbulk) {
+    if ((reinterpret_cast<uintptr_t>(q) & 15) == 0)
+      deep_bulk<true>(L, wave, lane, q, nbulk, do_sha, do_crc, h, crc_raw);
+    else
+      deep_bulk<false>(L, wave, lane, q, nbulk, do_sha, do_crc, h, crc_raw);
+  }
+
+  // ---- tail (sha1.go:75-77): x[:r] = rest; x[r:] keeps stale bytes
+  const uint64_t tpos = pos + (nbulk << 6);
+  const uint32_t r = (uint32_t)(plen - tpos);
+  if (do_crc)
+    for (uint32_t i = 0; i < r; ++i) crc_raw = crc_byte(L.tab.slice8[0], crc_raw, p[tpos + i]);
+  if (do_sha && r > 0) {
+    if ((uint32_t)lane < r) xs[lane] = p[tpos + lane];
+    nx_new = r;
+  }
+  wave_lds_sync();
+  len += plen;  // sha1.go:60
+
+  // ---- Sum (sha1.go:89-120) on a copy of the state
+  uint32_t dig[5] = {0, 0, 0, 0, 0};
+  bool have_sum = false;
+  if (fin && do_sha) {
+    const uint32_t nxf = nx_new > 0 ? (uint32_t)nx_new : 0u;  // Write skips a negative nx (sha1.go:61)
+    const uint32_t lm = (uint32_t)(len & 63);
+    const uint32_t padlen = lm < 56 ? 56 - lm : 120 - lm;     // sha1.go:94-98
+    const uint32_t T = nxf + padlen + 8;
+    if (T & 63) {
+      status = EFES_ERR_STATE;  // sha1.go:107-109 panic("d.nx != 0")
+    } else {
+      uint8_t* fb = L.fin[wave];
+      const uint64_t bits = len << 3;
+      for (uint32_t i = lane; i < T; i += 64) {
+        uint32_t b;
+        if (i < nxf) b = xs[i];
+        else if (i == nxf) b = 0x80;
+        else if (i >= T - 8) b = (uint32_t)(bits >> (56 - 8 * (i - (T - 8)))) & 0xffu;
+        else b = 0;
+        fb[i] = (uint8_t)b;
+      }
+      wave_lds_sync();
+      uint32_t hf[5] = {h[0], h[1], h[2], h[3], h[4]};
+      for (uint32_t blk = 0; blk < T / 64; ++blk) {
+        uint32_t w[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) w[k] = be_word_lds(fb + 64 * blk, k);
+        compress_inline(hf, w);
+      }
+#pragma unroll
+      for (int k = 0; k < 5; ++k) dig[k] = hf[k];
+      have_sum = true;
+    }
+  }
+
+  // ---- write back
+  if (do_sha) {
+    if (lane < 5) {
+      uint32_t v = h[0];
+#pragma unroll
+      for (int k = 1; k < 5; ++k) v = lane == k ? h[k] : v;
+      J.st->h[lane] = v;
+    }
+    if (lane < 16) reinterpret_cast<uint32_t*>(J.st->x)[lane] = reinterpret_cast<const uint32_t*>(xs)[lane];
+    if (lane == 0) {
+      J.st->nx = nx_new;
+      J.st->len = len;
+    }
+  }
+  if (do_crc && lane == 0) J.cs->crc = ~crc_raw;
+  if (fin && J.sum && lane < 6) {
+    uint32_t v;
+    if (lane < 5) {
+      v = dig[0];
+#pragma unroll
+      for (int k = 1; k < 5; ++k) v = lane == k ? dig[k] : v;
+      v = have_sum ? v : 0u;
+    } else {
+      v = do_crc ? ~crc_raw : 0u;
+    }
+    reinterpret_cast<uint32_t*>(J.sum)[lane] = bswap(v);  // big-endian, as Sum appends
+  }
+  if (lane == 0 && J.status) *J.status = status;
+}
+
+__global__ __launch_bounds__(64 * kDeepWaves, 1) void deep_kernel(const efes_job* __restrict__ jobs, uint32_t njobs,
+                                                                  const Tables* __restrict__ tabs) {
+  __shared__ __attribute__((aligned(16))) DeepLDS L;
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(tabs);
+    uint4* dst = reinterpret_cast<uint4*>(&L.tab);
+    for (int i = threadIdx.x; i < (int)(sizeof(Tables) / 16); i += blockDim.x) dst[i] = src[i];
+  }
+  __syncthreads();
+  const int wave = (int)uniform32(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const uint32_t j = blockIdx.x * kDeepWaves + (uint32_t)wave;
+  if (j >= njobs) return;
+  const efes_job* jb = jobs + j;
+  DeepJob J;
+  J.p = reinterpret_cast<const uint8_t*>(uniform64(reinterpret_cast<uint64_t>(jb->data)));
+  J.plen = uniform64(jb->length);
+  J.st = reinterpret_cast<efes_sha1_state*>(uniform64(reinterpret_cast<uint64_t>(jb->sha1)));
+  J.cs = reinterpret_cast<efes_crc32_state*>(uniform64(reinterpret_cast<uint64_t>(jb->crc32)));
+  J.sum = reinterpret_cast<uint8_t*>(uniform64(reinterpret_cast<uint64_t>(jb->sum)));
+  J.status = reinterpret_cast<int32_t*>(uniform64(reinterpret_cast<uint64_t>(jb->status)));
+  J.flags = uniform32(jb->flags);
+  deep_job(L, wave, lane, J);
+}
+
+// ================================================================== WIDE kernel
+// One lane per job.  Per-lane tail buffers live in LDS with a 68-byte stride (17 dwords:
+// lanes touching the same byte index hit different banks).
+constexpr int kWideWaves = 4;
+constexpr int kXStride = 68;
+
+struct WideLDS {
+  uint32_t slice8[8][256];
+  uint8_t xs[kWideWaves * 64][kXStride];
+};
+
+// Byte i of the padded final stream x[:nxf] || 0x80 || 0.. || BE64(bits), length T.
+__device__ __forceinline__ uint32_t fin_byte(const uint8_t* xl, uint32_t i, uint32_t nxf, uint32_t T, uint64_t bits) {
+  if (i < nxf) return xl[i];
+  if (i == nxf) return 0x80u;
+  if (i >= T - 8) return (uint32_t)(bits >> (56 - 8 * (i - (T - 8)))) & 0xffu;
+  return 0u;
+}
+
+__global__ __launch_bounds__(64 * kWideWaves, 2) void wide_kernel(const efes_job* __restrict__ jobs, uint32_t njobs,
+                                                                  const Tables* __restrict__ tabs) {
+  __shared__ __attribute__((aligned(16))) WideLDS L;
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(tabs->slice8);
+    uint4* dst = reinterpret_cast<uint4*>(L.slice8);
+    for (int i = threadIdx.x; i < (int)(sizeof(L.slice8) / 16); i += blockDim.x) dst[i] = src[i];
+  }
+  __syncthreads();
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool live = j < njobs;
+  const efes_job jb = live ? jobs[j] : efes_job{};
+  const uint8_t* p = reinterpret_cast<const uint8_t*>(jb.data);
+  const uint64_t plen = jb.length;
+  efes_sha1_state* st = jb.sha1;
+  efes_crc32_state* cs = jb.crc32;
+  const bool do_sha = live && st != nullptr, do_crc = live && cs != nullptr;
+  const bool fin = live && (jb.flags & EFES_JOB_FINALIZE) != 0;
+  uint8_t* xl = L.xs[threadIdx.x];
+  int32_t status = EFES_OK;
+
+  uint32_t h[5] = {0, 0, 0, 0, 0};
+  int64_t nx = 0;
+  uint64_t len = 0;
+  if (do_sha) {
+#pragma unroll
+    for (int k = 0; k < 5; ++k) h[k] = st->h[k];
+    nx = st->nx;
+    len = st->len;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const uint32_t v = reinterpret_cast<const uint32_t*>(st->x)[k];
+      xl[4 * k] = (uint8_t)v; xl[4 * k + 1] = (uint8_t)(v >> 8); xl[4 * k + 2] = (uint8_t)(v >> 16); xl[4 * k + 3] = (uint8_t)(v >> 24);
+    }
+  }
+  uint32_t crc_raw = do_crc ? ~cs->crc : 0u;
+  const bool bad = do_sha && nx > 64;  // sha1.go:62 panic
+  const bool go = live && !bad;
+
+  // ---- head
+  uint64_t pos = 0;
+  int64_t nx_new = nx;
+  if (go && do_sha && nx > 0) {
+    const uint32_t room = (uint32_t)(64 - nx);
+    const uint32_t nh = plen < room ? (uint32_t)plen : room;
+    for (uint32_t i = 0; i < nh; ++i) xl[nx + i] = p[i];
+    if ((uint32_t)nx + nh == 64) {
+      uint32_t w[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) w[k] = be_word_lds(xl, k);
+      compress_inline(h, w);
+      nx_new = 0;
+    } else {
+      nx_new = nx + nh;
+    }
+    pos = nh;
+  }
+  if (go && do_crc)
+    for (uint64_t i = 0; i < pos; ++i) crc_raw = crc_byte(L.slice8[0], crc_raw, p[i]);
+
+  // ---- bulk: lanes iterate their own block counts (masked when done)
+  const uint8_t* q = p + pos;
+  const uint64_t nbulk = go ? (plen - pos) >> 6 : 0;
+  const bool all16 = __all(!go || (reinterpret_cast<uintptr_t>(q) & 15) == 0);
+  for (uint64_t b = 0; b < nbulk; ++b) {
+    uint32_t le[16];
+    if (all16) load_block_le<true>(q + 64 * b, le);
+    else load_block_le<false>(q + 64 * b, le);
+    if (do_crc) crc_raw = crc_words_raw(L.slice8, crc_raw, le);
+    if (do_sha) {
+      uint32_t w[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) w[k] = bswap(le[k]);
+      compress_inline(h, w);
+    }
+  }
+
+  // ---- tail
+  const uint64_t tpos = pos + (nbulk << 6);
+  const uint32_t r = go ? (uint32_t)(plen - tpos) : 0u;
+  if (do_crc)
+    for (uint32_t i = 0; i < r; ++i) crc_raw = crc_byte(L.slice8[0], crc_raw, p[tpos + i]);
+  if (do_sha && r > 0) {
+    for (uint32_t i = 0; i < r; ++i) xl[i] = p[tpos + i];
+    nx_new = r;
+  }
+  len += go ? plen : 0;
+
+  // ---- Sum
+  uint32_t dig[5] = {0, 0, 0, 0, 0};
+  if (go && fin && do_sha) {
+    const uint32_t nxf = nx_new > 0 ? (uint32_t)nx_new : 0u;
+    const uint32_t lm = (uint32_t)(len & 63);
+    const uint32_t padlen = lm < 56 ? 56 - lm : 120 - lm;
+    const uint32_t T = nxf + padlen + 8;
+    if (T & 63) {
+      status = EFES_ERR_STATE;
+    } else {
+      const uint64_t bits = len << 3;
+      uint32_t hf[5] = {h[0], h[1], h[2], h[3], h[4]};
+      for (uint32_t blk = 0; blk < T / 64; ++blk) {
+        uint32_t w[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          const uint32_t i = 64 * blk + 4 * k;
+          w[k] = fin_byte(xl, i, nxf, T, bits) << 24 | fin_byte(xl, i + 1, nxf, T, bits) << 16 |
+                 fin_byte(xl, i + 2, nxf, T, bits) << 8 | fin_byte(xl, i + 3, nxf, T, bits);
+        }
+        compress_inline(hf, w);
+      }
+#pragma unroll
+      for (int k = 0; k < 5; ++k) dig[k] = hf[k];
+    }
+  }
+
+  // ---- write back
+  if (go) {
+    if (do_sha) {
+#pragma unroll
+      for (int k = 0; k < 5; ++k) st->h[k] = h[k];
+#pragma unroll
+      for (int k = 0; k < 16; ++k)
+        reinterpret_cast<uint32_t*>(st->x)[k] = (uint32_t)xl[4 * k] | (uint32_t)xl[4 * k + 1] << 8 |
+                                                (uint32_t)xl[4 * k + 2] << 16 | (uint32_t)xl[4 * k + 3] << 24;
+      st->nx = nx_new;
+      st->len = len;
+    }
+    if (do_crc) cs->crc = ~crc_raw;
+    if (fin && jb.sum) {
+#pragma unroll
+      for (int k = 0; k < 5; ++k) reinterpret_cast<uint32_t*>(jb.sum)[k] = bswap(status == EFES_OK ? dig[k] : 0u);
+      reinterpret_cast<uint32_t*>(jb.sum)[5] = bswap(do_crc ? ~crc_raw : 0u);
+    }
+  }
+  if (live && jb.status) *jb.status = bad ? EFES_ERR_STATE : status;
+}
+
+// ================================================================== synthetic fill
+__device__ __forceinline__ uint64_t splitmix(uint64_t seed, uint64_t i) {
+  uint64_t z = seed + (i + 1) * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__global__ void fill_kernel(uint64_t* __restrict__ dst, uint64_t nwords, uint64_t seed, uint8_t* tail_dst,
+                            uint32_t tail_bytes) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nwords; i += stride) dst[i] = splitmix(seed, i);
+  if (blockIdx.x == 0 && threadIdx.x == 0 && tail_bytes) {
+    const uint64_t z = splitmix(seed, nwords);
+    for (uint32_t b = 0; b < tail_bytes; ++b) tail_dst[b] = (uint8_t)(z >> (8 * b));
+  }
+}
+
+// ================================================================== launchers
+hipError_t launch_deep(const efes_job* jobs, uint32_t njobs, const Tables* tabs, hipStream_t s) {
+  if (njobs == 0) return hipSuccess;
+  const uint32_t grid = (njobs + kDeepWaves - 1) / kDeepWaves;
+  hipLaunchKernelGGL(deep_kernel, dim3(grid), dim3(64 * kDeepWaves), 0, s, jobs, njobs, tabs);
+  return hipGetLastError();
+}
+
+hipError_t launch_wide(const efes_job* jobs, uint32_t njobs, const Tables* tabs, hipStream_t s) {
+  if (njobs == 0) return hipSuccess;
+  const uint32_t per = 64 * kWideWaves;
+  hipLaunchKernelGGL(wide_kernel, dim3((njobs + per - 1) / per), dim3(per), 0, s, jobs, njobs, tabs);
+  return hipGetLastError();
+}
+
+hipError_t launch_fill(void* dst, size_t bytes, uint64_t seed, hipStream_t s) {
+  const uint64_t nwords = bytes / 8;
+  const uint32_t tail = (uint32_t)(bytes % 8);
+  uint64_t blocks = (nwords + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  if (blocks == 0) blocks = 1;
+  hipLaunchKernelGGL(fill_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, reinterpret_cast<uint64_t*>(dst), nwords,
+                     seed, reinterpret_cast<uint8_t*>(dst) + nwords * 8, tail);
+  return hipGetLastError();
+}
+
+}  // namespace efes

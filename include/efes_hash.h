@@ -1,0 +1,163 @@
+/*
+ * efes_hash.h -- C ABI of the MI355X-native content-hashing path of efes.
+ *
+ * This library replaces the per-chunk SHA-1 + CRC-32/IEEE that putdotio/efes streams
+ * every uploaded byte through.  Cited reference interfaces (/root/reference/<file>:<line>):
+ *   sha1digest  (sha1.go:29-120), its text codec (sha1_efes.go:25-64),
+ *   crc32digest (crc32.go:48-93), its text codec (crc32_efes.go:18-40),
+ *   and the hot loop io.MultiWriter(f, CRC32, Sha1) + io.Copy (filereceiver.go:208-209).
+ *
+ * Two layers:
+ *   1. Batched device-resident hot path (efes_hash_submit): every job is ONE `Write(p)`
+ *      (sha1.go:58-79 and crc32.go:76-86) of a device buffer into a device-resident
+ *      state, optionally followed by `Sum` (sha1.go:82-120, crc32.go:90-93).  All
+ *      compression runs in hand-written gfx950 kernels.  Jobs are independent.
+ *   2. Streaming digest objects mirroring the Go `hash.Hash` surface (efes_sha1_*,
+ *      efes_crc32_*), staging host bytes and hashing them on the GPU through layer 1.
+ *      Their MarshalText/UnmarshalText are byte-identical to the reference's, so
+ *      `<path>.info` files (fileinfo.go:10-58) stay interchangeable.
+ *
+ * Plain C types only; every pointer documented "device" must be device memory of the
+ * context's GPU (hipMalloc), "host" pointers are ordinary host memory.  Functions
+ * return 0 (EFES_OK) or a negative efes error code; nothing panics or aborts.
+ * All functions are thread-safe except concurrent use of ONE streaming object.
+ */
+#ifndef EFES_HASH_H
+#define EFES_HASH_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define EFES_ABI_VERSION 1
+
+/* ---- error codes ---------------------------------------------------------------- */
+#define EFES_OK 0
+#define EFES_ERR_INVALID_DIGEST (-1) /* sha1_efes.go:23 errInvalidDigest (bad text length / hex) */
+#define EFES_ERR_STATE (-2)          /* state on which the Go code would panic: nx > 64 at Write
+                                        (slice bounds, sha1.go:62) or d.nx != 0 in checkSum (sha1.go:107-109) */
+#define EFES_ERR_HIP (-3)            /* a HIP runtime call failed (device fault, OOM, ...) */
+#define EFES_ERR_ARG (-4)            /* invalid argument (NULL, bad flags, misaligned state) */
+#define EFES_ERR_NO_DEVICE (-5)      /* no usable gfx950 device */
+#define EFES_ERR_NOMEM (-6)          /* host allocation failed */
+#define EFES_ERR_DEVICE_FAULT (-7)   /* an earlier asynchronous device error was latched */
+
+const char* efes_strerror(int code);
+int efes_abi_version(void);
+
+/* ---- state layouts (device- and host-side identical) ----------------------------- */
+
+/* sha1.go:29-34 `sha1digest`: field order = MarshalText order (sha1_efes.go:26-34). */
+typedef struct efes_sha1_state {
+    uint32_t h[5];  /* running hash */
+    uint8_t x[64];  /* tail buffer; bytes x[nx:64] are stale, exactly as in Go */
+    uint32_t _pad;  /* keeps nx/len 8-byte aligned; ignored */
+    int64_t nx;     /* bytes pending in x (Go int) */
+    uint64_t len;   /* total bytes written (Go uint64, wraps) */
+} efes_sha1_state; /* 104 bytes */
+
+/* crc32.go:48-51 `crc32digest` (the table is always IEEE, crc32_efes.go:37-38). */
+typedef struct efes_crc32_state {
+    uint32_t crc; /* the finalized CRC-32/IEEE of everything written so far (Sum32) */
+} efes_crc32_state;
+
+/* sha1.go:36-44 Reset / sha1.go:48-52 NewSha1. */
+void efes_sha1_state_init(efes_sha1_state* s);
+
+/* ---- context ----------------------------------------------------------------------- */
+typedef struct efes_ctx efes_ctx;
+
+/* Binds one GPU (HIP device ordinal), uploads the CRC tables, creates a stream. */
+int efes_ctx_create(int device, efes_ctx** out);
+void efes_ctx_destroy(efes_ctx* ctx);
+int efes_ctx_device(const efes_ctx* ctx);
+/* The context's own stream (a hipStream_t), used when a call passes stream == NULL. */
+void* efes_ctx_stream(efes_ctx* ctx);
+
+/* ---- layer 1: batched device-resident jobs ----------------------------------------- */
+#define EFES_JOB_FINALIZE 0x1u /* also write Sum of the post-Write state to `sum` */
+
+/* One `Write(p)` (+ optional Sum) of len(p) = length bytes at device address `data`.
+ * sha1 / crc32: device states updated in place; either may be NULL to skip that hash
+ * (the MultiWriter of filereceiver.go:208 passes both).  sum (device, 24 bytes, only
+ * with EFES_JOB_FINALIZE): SHA-1 Sum (20 B, sha1.go:82-87) then CRC-32 Sum (4 B BE,
+ * crc32.go:90-93).  status (device, may be NULL): EFES_OK or EFES_ERR_STATE.
+ * Jobs in one submit must not share a state. */
+typedef struct efes_job {
+    const void* data;
+    uint64_t length;
+    efes_sha1_state* sha1;
+    efes_crc32_state* crc32;
+    uint8_t* sum;
+    int32_t* status;
+    uint32_t flags;
+    uint32_t _reserved;
+} efes_job; /* 56 bytes */
+
+/* Kernel shapes: DEEP = one wavefront per job (few, long jobs: per-job latency bound);
+ * WIDE = one lane per job (many jobs: throughput bound).  AUTO picks by njobs. */
+#define EFES_MODE_AUTO 0
+#define EFES_MODE_DEEP 1
+#define EFES_MODE_WIDE 2
+
+/* Enqueue njobs jobs (the job array itself in DEVICE memory) on `stream` (a
+ * hipStream_t; NULL = the context stream).  Asynchronous; returns launch errors only. */
+int efes_hash_submit(efes_ctx* ctx, const efes_job* jobs_device, uint32_t njobs, void* stream);
+int efes_hash_submit_mode(efes_ctx* ctx, const efes_job* jobs_device, uint32_t njobs, void* stream, int mode);
+/* Wait for `stream` (NULL = context stream); reports latched asynchronous errors. */
+int efes_sync(efes_ctx* ctx, void* stream);
+
+/* Device memory helpers for hosts without their own allocator (cgo). */
+int efes_device_alloc(efes_ctx* ctx, size_t bytes, void** out);
+int efes_device_free(efes_ctx* ctx, void* p);
+int efes_copy_to_device(efes_ctx* ctx, void* dst_device, const void* src_host, size_t bytes, void* stream);
+int efes_copy_to_host(efes_ctx* ctx, void* dst_host, const void* src_device, size_t bytes, void* stream);
+/* Synthetic benchmark bytes: little-endian splitmix64 stream, z_i = mix(seed + (i+1)*0x9E3779B97F4A7C15). */
+int efes_fill_synthetic(efes_ctx* ctx, void* dst_device, size_t bytes, uint64_t seed, void* stream);
+
+/* ---- layer 2: streaming digests mirroring the Go surface ---------------------------- */
+typedef struct efes_sha1 efes_sha1;
+typedef struct efes_crc32 efes_crc32;
+
+int efes_sha1_new(efes_ctx* ctx, efes_sha1** out);                       /* sha1.go:48-52 NewSha1 */
+int efes_sha1_new_zero(efes_ctx* ctx, efes_sha1** out);                  /* `var d sha1digest` (zero value) */
+void efes_sha1_free(efes_sha1* d);
+void efes_sha1_reset(efes_sha1* d);                                      /* sha1.go:36-44 */
+int efes_sha1_size(void);                                                /* sha1.go:54 (20) */
+int efes_sha1_block_size(void);                                          /* sha1.go:56 (64) */
+int efes_sha1_write(efes_sha1* d, const void* p, size_t n);              /* sha1.go:58-79 */
+int efes_sha1_sum(efes_sha1* d, uint8_t out[20]);                        /* sha1.go:82-87 */
+int efes_sha1_marshal_text(efes_sha1* d, char out[200]);                 /* sha1_efes.go:25-38 */
+int efes_sha1_unmarshal_text(efes_sha1* d, const char* text, size_t n);  /* sha1_efes.go:40-64 */
+int efes_sha1_get_state(efes_sha1* d, efes_sha1_state* out);
+int efes_sha1_set_state(efes_sha1* d, const efes_sha1_state* in);
+
+int efes_crc32_new(efes_ctx* ctx, efes_crc32** out);                     /* crc32.go:68 NewCRC32IEEE */
+void efes_crc32_free(efes_crc32* d);
+void efes_crc32_reset(efes_crc32* d);                                    /* crc32.go:74 */
+int efes_crc32_size(void);                                               /* crc32.go:70 (4) */
+int efes_crc32_block_size(void);                                         /* crc32.go:72 (1) */
+int efes_crc32_write(efes_crc32* d, const void* p, size_t n);            /* crc32.go:76-86 */
+int efes_crc32_sum32(efes_crc32* d, uint32_t* out);                      /* crc32.go:88 */
+int efes_crc32_sum(efes_crc32* d, uint8_t out[4]);                       /* crc32.go:90-93 */
+int efes_crc32_marshal_text(efes_crc32* d, char out[8]);                 /* crc32_efes.go:18-24 */
+int efes_crc32_unmarshal_text(efes_crc32* d, const char* text, size_t n);/* crc32_efes.go:26-40 */
+
+/* Host-side diagnostics (no device work): copies the CRC-32 tables the kernels use,
+ * slice8[8][256] (crc32.go:138-149) then shift[7][4][256] (advance of the raw register
+ * over 64<<k zero bytes, byte-sliced); returns the word count written or EFES_ERR_ARG. */
+int efes_crc32_tables(uint32_t* out, size_t nwords);
+
+/* Pure text codecs on plain states (no device work). */
+void efes_sha1_state_marshal_text(const efes_sha1_state* s, char out[200]);
+int efes_sha1_state_unmarshal_text(efes_sha1_state* s, const char* text, size_t n);
+void efes_crc32_state_marshal_text(const efes_crc32_state* s, char out[8]);
+int efes_crc32_state_unmarshal_text(efes_crc32_state* s, const char* text, size_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* EFES_HASH_H */

@@ -1,0 +1,120 @@
+"""The C ABI boundary (include/efes_hash.h) without a GPU: exports, layouts, host codecs, tables."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "efes_hash.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(efes_\w+)\s*\(", src)))
+
+
+def test_every_declared_symbol_is_exported(efes_lib):
+    L = ctypes.CDLL(efes_lib.LIB_PATH)
+    names = declared_functions()
+    assert len(names) >= 40
+    missing = [n for n in names if not hasattr(L, n)]
+    assert not missing, missing
+    # the Python binding declares a signature for every one of them
+    assert sorted(efes_lib.SIGNATURES) == names
+
+
+def test_nm_shows_c_linkage(efes_lib):
+    out = subprocess.run(["nm", "-D", "--defined-only", efes_lib.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r"\s[TW]\s+(efes_\w+)$", out, flags=re.M))
+    assert set(declared_functions()) <= exported
+
+
+def test_struct_layouts_match_header(tmp_path, efes_lib):
+    prog = tmp_path / "layout.c"
+    prog.write_text("""
+#include <stdio.h>
+#include <stddef.h>
+#include "efes_hash.h"
+int main(void) {
+  printf("%zu %zu %zu %zu %zu\\n", sizeof(efes_sha1_state), offsetof(efes_sha1_state, x),
+         offsetof(efes_sha1_state, nx), offsetof(efes_sha1_state, len), sizeof(efes_crc32_state));
+  printf("%zu %zu %zu %zu %zu %zu %zu %zu\\n", sizeof(efes_job), offsetof(efes_job, length), offsetof(efes_job, sha1),
+         offsetof(efes_job, crc32), offsetof(efes_job, sum), offsetof(efes_job, status), offsetof(efes_job, flags),
+         offsetof(efes_job, _reserved));
+  return 0;
+}""")
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.dirname(HEADER), str(prog), "-o", str(exe)], check=True)
+    a, b = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split("\n")[:2]
+    S, J = efes_lib.Sha1State, efes_lib.Job
+    assert a.split() == [str(v) for v in (ctypes.sizeof(S), S.x.offset, S.nx.offset, S.len.offset, 4)]
+    assert b.split() == [str(v) for v in (ctypes.sizeof(J), J.length.offset, J.sha1.offset, J.crc32.offset,
+                                          J.sum.offset, J.status.offset, J.flags.offset, J._reserved.offset)]
+    assert efes_lib.JOB_DTYPE.itemsize == ctypes.sizeof(J)
+    assert efes_lib.SHA1_STATE_DTYPE.fields["nx"][1] == S.nx.offset
+
+
+def test_host_codecs_match_golden(efes_lib, golden):
+    L = efes_lib.lib()
+    for case in golden["sha1_states"]:
+        for text in case["texts"]:
+            st = efes_lib.Sha1State()
+            assert L.efes_sha1_state_unmarshal_text(ctypes.byref(st), text.encode(), 200) == 0
+            out = ctypes.create_string_buffer(200)
+            L.efes_sha1_state_marshal_text(ctypes.byref(st), out)
+            assert out.raw.decode() == text
+    st = efes_lib.Sha1State()
+    assert L.efes_sha1_state_unmarshal_text(ctypes.byref(st), b"00" * 99, 198) == efes_lib.EFES_ERR_INVALID_DIGEST
+    assert L.efes_sha1_state_unmarshal_text(ctypes.byref(st), b"0g" * 100, 200) == efes_lib.EFES_ERR_INVALID_DIGEST
+    c = efes_lib.Crc32State()
+    assert L.efes_crc32_state_unmarshal_text(ctypes.byref(c), b"0d4a1185", 8) == 0 and c.crc == 0x0D4A1185
+    out = ctypes.create_string_buffer(8)
+    L.efes_crc32_state_marshal_text(ctypes.byref(c), out)
+    assert out.raw == b"0d4a1185"
+    assert L.efes_crc32_state_unmarshal_text(ctypes.byref(c), b"0d4a118", 7) == efes_lib.EFES_ERR_INVALID_DIGEST
+
+
+def test_state_init_is_newsha1(efes_lib):
+    st = efes_lib.Sha1State()
+    st.nx, st.len = 5, 9
+    efes_lib.lib().efes_sha1_state_init(ctypes.byref(st))
+    assert list(st.h) == [0x67452301, 0xEFCDAB89, 0x98BADCFE, 0x10325476, 0xC3D2E1F0] and st.nx == 0 and st.len == 0
+
+
+def _advance_raw(t0, s, nbytes):
+    for _ in range(nbytes):
+        s = int(t0[s & 0xFF]) ^ (s >> 8)
+    return s
+
+
+def test_crc_tables(efes_lib, oracle):
+    n = 8 * 256 + 7 * 4 * 256
+    buf = np.zeros(n, dtype=np.uint32)
+    assert efes_lib.lib().efes_crc32_tables(buf.ctypes.data, n) == n
+    slice8 = buf[:2048].reshape(8, 256)
+    for k in range(8):
+        assert (slice8[k] == oracle.crc32_table(k)).all()
+    shift = buf[2048:].reshape(7, 4, 256)
+    t0 = slice8[0]
+    rng = np.random.default_rng(0)
+    for k in range(7):
+        for v in [1, 0x80000000, int(rng.integers(0, 2**32))]:
+            got = 0
+            for b in range(4):
+                got ^= int(shift[k, b, (v >> (8 * b)) & 0xFF])
+            assert got == _advance_raw(t0, v, 64 << k), (k, hex(v))
+    assert efes_lib.lib().efes_crc32_tables(buf.ctypes.data, n - 1) == efes_lib.EFES_ERR_ARG
+
+
+def test_no_gpu_is_an_error_not_a_fallback(efes_lib):
+    torch = pytest.importorskip("torch")
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    h = ctypes.c_void_p()
+    rc = efes_lib.lib().efes_ctx_create(0, ctypes.byref(h))
+    assert rc == efes_lib.EFES_ERR_NO_DEVICE and not h.value
+    assert efes_lib.lib().efes_strerror(rc) == b"no usable gfx950 device"

@@ -1,0 +1,406 @@
+"""GPU parity: the gfx950 kernels (through the C ABI) against the CPU oracle and golden vectors.
+
+Bit-exact on everything: SHA-1 digests, CRC-32 values, and the full post-Write state
+(h, all 64 bytes of x including the stale tail, nx, len) that MarshalText serialises.
+"""
+import hashlib
+import io
+import random
+import zlib
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def env():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import efes_amd
+    from efes_amd import hashing
+    from efes_amd.batch import DeviceBatch, fresh_states
+    ctx = hashing.default_context(0)
+    return dict(torch=torch, efes=efes_amd, hashing=hashing, DeviceBatch=DeviceBatch, fresh_states=fresh_states,
+                ctx=ctx)
+
+
+MODE_IDS = ["deep", "wide"]
+
+
+def _modes(env):
+    return {"deep": env["efes"].MODE_DEEP, "wide": env["efes"].MODE_WIDE}
+
+
+def device_buffer(env, host: np.ndarray):
+    t = env["torch"].from_numpy(host).to("cuda:0")
+    env["torch"].cuda.synchronize()
+    return t
+
+
+def oracle_expect(oracle, state_row, data: bytes, crc_in: int, finalize: bool = True):
+    """Expected (status, state dict, crc, sha1 sum bytes|None) of one job per the CPU oracle."""
+    s = oracle.Sha1(reset=False)
+    s.st.h[:] = [int(v) for v in state_row["h"]]
+    s.st.x[:] = bytes(state_row["x"])
+    s.st.nx = int(state_row["nx"])
+    s.st.len = int(state_row["len"])
+    crc = zlib.crc32(data, crc_in)
+    rc = s.write(data)
+    if rc:
+        return -2, None, None, None
+    src, digest = s.sum()
+    if not finalize:
+        src = 0
+    return (0 if src == 0 else -2), dict(h=list(s.st.h), x=bytes(s.st.x), nx=s.st.nx, len=s.st.len), crc, \
+        (digest if src == 0 else None)
+
+
+def check_batch(b, oracle, datas, states, crcs, finalize=True, what=""):
+    status = b.status_host()
+    st = b.states_host()
+    crc = b.crc_sum()
+    sums = b.sums_host()
+    for i, data in enumerate(datas):
+        e_status, e_state, e_crc, e_sum = oracle_expect(oracle, states[i], data, int(crcs[i]), finalize)
+        assert status[i] == e_status, (what, i, len(data), status[i], e_status)
+        if e_state is None:
+            # Go panicked inside Write: nothing written back
+            assert list(st[i]["h"]) == list(states[i]["h"]) and st[i]["nx"] == states[i]["nx"], (what, i)
+            continue
+        assert list(st[i]["h"]) == e_state["h"], (what, i, len(data))
+        assert bytes(st[i]["x"]) == e_state["x"], (what, i, len(data))
+        assert int(st[i]["nx"]) == e_state["nx"] and int(st[i]["len"]) == e_state["len"], (what, i)
+        assert int(crc[i]) == e_crc, (what, i, len(data))
+        if finalize and e_sum is not None:
+            assert bytes(sums[i][:20]) == e_sum, (what, i, len(data))
+            assert bytes(sums[i][20:]) == e_crc.to_bytes(4, "big"), (what, i)
+
+
+@pytest.mark.parametrize("mode", MODE_IDS)
+def test_golden_synthetic_vectors(env, golden, oracle, mode):
+    vecs = golden["synthetic"]
+    stride = max(v["length"] for v in vecs) + 4096
+    stride = (stride + 4095) // 4096 * 4096
+    host = np.zeros(stride * len(vecs), dtype=np.uint8)
+    for i, v in enumerate(vecs):
+        host[i * stride:i * stride + v["length"]] = oracle.fill_synthetic(v["length"], v["seed"])
+    buf = device_buffer(env, host)
+    b = env["DeviceBatch"](buf.data_ptr(), [i * stride for i in range(len(vecs))], [v["length"] for v in vecs],
+                           ctx=env["ctx"])
+    b.run(_modes(env)[mode])
+    assert (b.status_host() == 0).all()
+    for v, sha, crc in zip(vecs, b.sha1_hex(), b.crc_sum()):
+        assert sha == v["sha1"], v["length"]
+        assert "%08x" % crc == v["crc32"], v["length"]
+
+
+@pytest.mark.parametrize("mode", MODE_IDS)
+def test_kat_strings(env, golden, mode):
+    vecs = golden["kat"]
+    stride = 1024
+    host = np.zeros(stride * len(vecs), dtype=np.uint8)
+    for i, v in enumerate(vecs):
+        b = v["text"].encode()
+        host[i * stride:i * stride + len(b)] = np.frombuffer(b, dtype=np.uint8)
+    buf = device_buffer(env, host)
+    b = env["DeviceBatch"](buf.data_ptr(), [i * stride for i in range(len(vecs))],
+                           [len(v["text"].encode()) for v in vecs], ctx=env["ctx"])
+    b.run(_modes(env)[mode])
+    for v, sha, crc in zip(vecs, b.sha1_hex(), b.crc_sum()):
+        assert sha == v["sha1"] and "%08x" % crc == v["crc32"], v["text"]
+
+
+@pytest.mark.parametrize("mode", MODE_IDS)
+def test_misaligned_offsets(env, oracle, mode):
+    rng = random.Random(11)
+    n = 96
+    lengths = [rng.choice([0, 1, 63, 64, 65, 200, 4095, 4096 + 3, 70000, 300001]) for _ in range(n)]
+    offsets, pos = [], 0
+    for L in lengths:
+        pos += rng.randint(0, 17)
+        offsets.append(pos)
+        pos += L
+    host = oracle.fill_synthetic(pos + 64, 321)
+    buf = device_buffer(env, host)
+    states = env["fresh_states"](n)
+    b = env["DeviceBatch"](buf.data_ptr(), offsets, lengths, ctx=env["ctx"])
+    b.run(_modes(env)[mode])
+    datas = [host[o:o + L].tobytes() for o, L in zip(offsets, lengths)]
+    check_batch(b, oracle, datas, states, np.zeros(n, np.uint32), what="misaligned")
+
+
+def midstream_states(oracle, env, n, rng):
+    """States after a random prefix write (nx in 0..63, stale x bytes), plus random CRC states."""
+    states = env["fresh_states"](n)
+    crcs = np.zeros(n, np.uint32)
+    for i in range(n):
+        s = oracle.Sha1()
+        for _ in range(rng.randint(0, 3)):
+            s.write(bytes(rng.getrandbits(8) for _ in range(rng.randint(0, 150))))
+        states[i]["h"] = list(s.st.h)
+        states[i]["x"] = np.frombuffer(bytes(s.st.x), dtype=np.uint8)
+        states[i]["nx"] = s.st.nx
+        states[i]["len"] = s.st.len
+        crcs[i] = rng.getrandbits(32)
+    return states, crcs
+
+
+@pytest.mark.parametrize("mode", MODE_IDS)
+@pytest.mark.parametrize("finalize", [True, False])
+def test_midstream_states(env, oracle, mode, finalize):
+    rng = random.Random(7 + finalize)
+    n = 80
+    states, crcs = midstream_states(oracle, env, n, rng)
+    lengths = [rng.choice([0, 1, 5, 31, 63, 64, 65, 127, 128, 129, 1000, 4096 * 64 + 9, 131072]) for _ in range(n)]
+    stride = 262144 + 4096
+    host = oracle.fill_synthetic(stride * n, 99)
+    buf = device_buffer(env, host)
+    offsets = [i * stride + (i % 5) for i in range(n)]
+    b = env["DeviceBatch"](buf.data_ptr(), offsets, lengths, states=states, crcs=crcs, finalize=finalize,
+                           ctx=env["ctx"])
+    b.run(_modes(env)[mode])
+    datas = [host[o:o + L].tobytes() for o, L in zip(offsets, lengths)]
+    check_batch(b, oracle, datas, states, crcs, finalize=finalize, what=f"midstream-{mode}")
+
+
+@pytest.mark.parametrize("mode", MODE_IDS)
+def test_go_quirk_states(env, oracle, mode):
+    """nx == 64 (full pending block), negative nx, nx > 64 (Go panics), nx inconsistent with len."""
+    fresh = env["fresh_states"]
+    cases = []  # (state, data)
+    s = fresh(1)[0].copy()
+    s["x"] = np.frombuffer(b"A" * 64, dtype=np.uint8); s["nx"] = 64; s["len"] = 64
+    cases += [(s, b""), (s, b"tail"), (s, b"z" * 200)]
+    s2 = fresh(1)[0].copy(); s2["nx"] = -7; s2["len"] = 3
+    cases += [(s2, b""), (s2, b"q" * 70), (s2, b"q" * 64)]
+    s3 = fresh(1)[0].copy(); s3["nx"] = 65
+    cases += [(s3, b""), (s3, b"abc")]
+    s4 = fresh(1)[0].copy(); s4["nx"] = 3; s4["len"] = 0; s4["x"][:3] = [1, 2, 3]
+    cases += [(s4, b""), (s4, b"x" * 61), (s4, b"x" * 200)]
+    s5 = fresh(1)[0].copy(); s5["nx"] = 0; s5["len"] = (1 << 64) - 5  # length wraps
+    cases += [(s5, b"wrap-around!")]
+    n = len(cases)
+    states = fresh(n)
+    for i, (st, _) in enumerate(cases):
+        states[i] = st
+    stride = 256
+    host = np.zeros(stride * n, dtype=np.uint8)
+    for i, (_, d) in enumerate(cases):
+        host[i * stride:i * stride + len(d)] = np.frombuffer(d, dtype=np.uint8)
+    buf = device_buffer(env, host)
+    b = env["DeviceBatch"](buf.data_ptr(), [i * stride for i in range(n)], [len(d) for _, d in cases],
+                           states=states, ctx=env["ctx"])
+    b.run(_modes(env)[mode])
+    check_batch(b, oracle, [d for _, d in cases], states, np.zeros(n, np.uint32), what=f"quirks-{mode}")
+
+
+@pytest.mark.parametrize("mode", MODE_IDS)
+def test_sha_only_and_crc_only(env, oracle, mode):
+    n = 10
+    lengths = [0, 1, 64, 100, 5000, 65, 63, 4096, 8191, 12345]
+    stride = 16384
+    host = oracle.fill_synthetic(stride * n, 5)
+    buf = device_buffer(env, host)
+    offs = [i * stride for i in range(n)]
+    b1 = env["DeviceBatch"](buf.data_ptr(), offs, lengths, crc32=False, ctx=env["ctx"])
+    b1.run(_modes(env)[mode])
+    b2 = env["DeviceBatch"](buf.data_ptr(), offs, lengths, sha1=False, ctx=env["ctx"])
+    b2.run(_modes(env)[mode])
+    for i, (o, L) in enumerate(zip(offs, lengths)):
+        d = host[o:o + L].tobytes()
+        assert b1.sha1_hex()[i] == hashlib.sha1(d).hexdigest()
+        assert bytes(b1.sums_host()[i][20:]) == b"\0\0\0\0"
+        assert b2.crc_sum()[i] == zlib.crc32(d)
+        assert bytes(b2.sums_host()[i][:20]) == b"\0" * 20
+        assert bytes(b2.sums_host()[i][20:]) == zlib.crc32(d).to_bytes(4, "big")
+
+
+def test_zero_jobs(env):
+    env["ctx"].submit(0, 0)
+    env["ctx"].sync()
+
+
+def test_many_small_jobs_auto_wide(env, oracle):
+    rng = np.random.default_rng(2)
+    n = 5000
+    lengths = rng.integers(0, 3000, n)
+    offsets = np.concatenate([[0], np.cumsum(lengths)[:-1]])
+    host = oracle.fill_synthetic(int(lengths.sum()) + 8, 1234)
+    buf = device_buffer(env, host)
+    b = env["DeviceBatch"](buf.data_ptr(), offsets, lengths, ctx=env["ctx"])
+    b.run()  # AUTO -> WIDE at this count
+    assert (b.status_host() == 0).all()
+    shas, crcs = b.sha1_hex(), b.crc_sum()
+    for i in range(0, n, 7):
+        d = host[offsets[i]:offsets[i] + lengths[i]].tobytes()
+        assert shas[i] == hashlib.sha1(d).hexdigest() and crcs[i] == zlib.crc32(d)
+
+
+@pytest.mark.parametrize("mode", MODE_IDS)
+def test_chunked_resume_equals_one_shot(env, golden, oracle, mode):
+    """A 4 MiB+1 object sent as PATCH chunks (write.go:126, filereceiver.go:182-226): state carried on device."""
+    v = next(v for v in golden["synthetic"] if v["length"] == (4 << 20) + 1)
+    host = oracle.fill_synthetic(v["length"], v["seed"])
+    buf = device_buffer(env, host)
+    torch = env["torch"]
+    cuts = [0, 1, 1000, 1 << 20, (1 << 20) + 63, 3 << 20, v["length"]]
+    states = env["fresh_states"](1)
+    crc = np.zeros(1, np.uint32)
+    for a, c in zip(cuts[:-1], cuts[1:]):
+        last = c == v["length"]
+        b = env["DeviceBatch"](buf.data_ptr(), [a], [c - a], states=states, crcs=crc, finalize=last, ctx=env["ctx"])
+        b.run(_modes(env)[mode])
+        states = b.states_host().copy()
+        crc = b.crc_sum().copy()
+    assert b.sha1_hex()[0] == v["sha1"]
+    assert "%08x" % crc[0] == v["crc32"]
+    del torch
+
+
+def test_4mib_batch_against_threaded_oracle(env, oracle):
+    n, size = 48, 4 << 20
+    torch = env["torch"]
+    buf = torch.empty(n * size, dtype=torch.uint8, device="cuda:0")
+    env["ctx"].fill_synthetic(buf.data_ptr(), buf.numel(), 0xEFE5, torch.cuda.current_stream().cuda_stream)
+    b = env["DeviceBatch"](buf.data_ptr(), [i * size for i in range(n)], [size] * n, ctx=env["ctx"])
+    b.run(env["efes"].MODE_DEEP)
+    host = buf.cpu().numpy()
+    _, sha, crc = oracle.hash_many(host, size, np.full(n, size), 8)
+    assert b.sha1_hex() == [bytes(r).hex() for r in sha]
+    assert (b.crc_sum() == crc).all()
+    b.reset()
+    b.run(env["efes"].MODE_WIDE)
+    assert b.sha1_hex() == [bytes(r).hex() for r in sha]
+    assert (b.crc_sum() == crc).all()
+
+
+def test_device_fill_matches_host_generator(env, oracle):
+    torch = env["torch"]
+    for n, seed in [(8, 1), (1000, 2), (4097, 3), (1 << 20, 0xEFE5)]:
+        buf = torch.zeros(n + 8, dtype=torch.uint8, device="cuda:0")
+        env["ctx"].fill_synthetic(buf.data_ptr(), n, seed, torch.cuda.current_stream().cuda_stream)
+        got = buf.cpu().numpy()
+        assert got[:n].tobytes() == oracle.fill_synthetic(n, seed).tobytes()
+        assert not got[n:].any()
+
+
+# ---------------------------------------------------------------- streaming (Go surface)
+
+def test_streaming_state_vectors(env, golden):
+    """MarshalText after every Write equals Go's, stale x bytes included (sha1_efes.go:25-38)."""
+    h = env["hashing"]
+    for case in golden["sha1_states"]:
+        d = h.Sha1Digest(reset=case["reset"])
+        for w, text in zip(case["writes"], case["texts"]):
+            assert d.write(bytes.fromhex(w)) == len(w) // 2
+            assert d.marshal_text().decode() == text, case["name"]
+        assert d.sum().hex() == case["sum"], case["name"]
+
+
+def test_sha1_partial_digest(env):
+    """sha1_efes_test.go:8-29 through the GPU-backed digest."""
+    h = env["hashing"]
+    d = h.Sha1Digest(reset=False)
+    d.write(b"hello world")
+    hex1 = d.sum().hex()
+    text = d.marshal_text()
+    d2 = h.Sha1Digest(reset=False)
+    d2.unmarshal_text(text)
+    assert d2.sum().hex() == hex1 == "73e8730e5086d8ced928b654beeb0e5383f9be01"
+
+
+def test_crc32_partial_digest(env, golden):
+    """crc32_efes_test.go:8-29."""
+    h = env["hashing"]
+    for case in golden["crc32_states"]:
+        c = h.new_crc32_ieee()
+        for w, text in zip(case["writes"], case["texts"]):
+            c.write(bytes.fromhex(w))
+            assert c.marshal_text().decode() == text
+        c2 = h.new_crc32_ieee()
+        c2.unmarshal_text(c.marshal_text())
+        assert c2.sum32() == c.sum32() == case["sum32"]
+        assert c2.sum() == case["sum32"].to_bytes(4, "big")
+
+
+def test_sum_is_non_destructive_and_appends(env):
+    h = env["hashing"]
+    d = h.new_sha1()
+    d.write(b"foo")
+    assert d.sum(b"prefix") == b"prefix" + hashlib.sha1(b"foo").digest()
+    d.write(b"bar")
+    assert d.sum().hex() == "8843d7f92416211de9ebb963ff4ce28125932878"  # TestFileReceiver foo+bar
+    assert d.size() == 20 and d.block_size() == 64
+
+
+def test_reset_keeps_stale_x_like_go(env):
+    """sha1.go:36-44: Reset does not clear x, so MarshalText still shows the old tail bytes."""
+    h = env["hashing"]
+    d = h.new_sha1()
+    d.write(b"stale bytes here")
+    d.reset()
+    text = d.marshal_text().decode()
+    assert text[:40] == "67452301efcdab8998badcfe10325476c3d2e1f0"
+    assert bytes.fromhex(text[40:40 + 32]) == b"stale bytes here"
+    assert text[168:] == "0" * 32
+    d.write(b"abc")
+    assert d.sum().hex() == hashlib.sha1(b"abc").hexdigest()
+
+
+def test_streaming_errors(env):
+    h = env["hashing"]
+    efes = env["efes"]
+    d = h.new_sha1()
+    with pytest.raises(efes.EfesError) as e:
+        d.unmarshal_text(b"00" * 99)
+    assert e.value.code == efes.EFES_ERR_INVALID_DIGEST
+    good = d.marshal_text()
+    d.unmarshal_text(good[:168] + b"%016x" % 65 + b"%016x" % 0)
+    with pytest.raises(efes.EfesError) as e:
+        d.write(b"x")
+    assert e.value.code == efes.EFES_ERR_STATE
+    d.unmarshal_text(good[:168] + b"%016x" % 3 + b"%016x" % 0)
+    with pytest.raises(efes.EfesError) as e:
+        d.sum()
+    assert e.value.code == efes.EFES_ERR_STATE
+    c = h.new_crc32_ieee()
+    with pytest.raises(efes.EfesError):
+        c.unmarshal_text(b"xyz")
+
+
+def test_sha1file_script(env, golden):
+    """sha1file_test.go:10-41 with the GPU-backed digest."""
+    f = golden["sha1file"]
+    sf = env["hashing"].Sha1File(io.BytesIO(f["content"].encode()))
+    for (seek, n), want in zip(f["script"], f["reads"]):
+        assert sf.seek(seek) == seek
+        assert sf.read(n).decode() == want
+    assert sf.sum().hex() == f["sha1"] == "5d2781d78fa5a97b7bafa849fe933dfc9dc93eba"
+
+
+def test_fileinfo_json_roundtrip(env):
+    """fileinfo.go: offset + digest JSON persisted between PATCHes, resumed, finalized."""
+    h = env["hashing"]
+    data = bytes(range(256)) * 40
+    fi = h.FileInfo()
+    fi.digest.write(data[:5000])
+    fi.offset = 5000
+    s = fi.dumps()
+    fi2 = h.FileInfo.loads(s)
+    assert fi2.offset == 5000
+    fi2.digest.write(data[5000:])
+    assert fi2.digest.sha1.sum().hex() == hashlib.sha1(data).hexdigest()
+    assert fi2.digest.crc32.sum32() == zlib.crc32(data)
+
+
+def test_large_streaming_write_flushes(env):
+    h = env["hashing"]
+    rng = np.random.default_rng(9)
+    data = rng.integers(0, 256, (64 << 20) + 777, dtype=np.uint8).tobytes()
+    d = h.new_sha1()
+    for i in range(0, len(data), 32 * 1024):  # io.Copy granularity
+        d.write(data[i:i + 32 * 1024])
+    assert d.sum().hex() == hashlib.sha1(data).hexdigest()

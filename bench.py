@@ -1,0 +1,210 @@
+#!/usr/bin/env python3
+"""bench.py -- GiB/s hashed (SHA-1 + CRC-32) on device-resident 4 MiB chunks, 1..N MI355X.
+
+Workload (BASELINE.json configs[2]): per GPU, 1024 independent 4 MiB chunks already resident
+in HBM; one step = one fused single-pass SHA-1 + CRC-32 over all of them, each chunk from a
+fresh NewSha1()/NewCRC32IEEE() state and finalised on device (the per-chunk digests that
+filereceiver.go:208-209 streams every uploaded byte through).  --sha1-only gives configs[1].
+
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): one process
+per GPU, each hashing its own 1024 chunks (weak scaling, per-GPU work queues, no data-path
+collective); a barrier + synchronize brackets the timed steps and the time is the max over
+ranks (one all_reduce of a scalar, timing only).
+
+Printed on rank 0: ONE JSON line with the driver's keys plus
+  roofline     -- the hashing kernel's algorithmic bytes per launch / its average launch time
+                  (HIP events on the launch stream), against the 8 TB/s HBM3E peak; traffic
+                  from profiles/<round>_traffic.json (rocprofv3 FETCH_SIZE pass) when present;
+  cpu_baseline -- the C restatement of the reference (oracle/, kind "port") over the same
+                  bytes on the host cores, N=1 rank 0 only, digests checked against the GPU's.
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+METRIC = "GiB/s hashed (SHA-1+CRC32), device-resident 4 MiB chunks, 1/2/4/8 MI355X"
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+GiB = 1 << 30
+
+
+def parse_args(argv=None):
+    p = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--chunks", type=int, default=1024, help="chunks per GPU")
+    p.add_argument("--chunk-bytes", type=int, default=4 << 20)
+    p.add_argument("--mode", choices=["auto", "deep", "wide"], default="auto")
+    p.add_argument("--sha1-only", action="store_true", help="BASELINE configs[1] (no CRC-32)")
+    p.add_argument("--cpu-threads", type=int, default=0, help="cpu_baseline threads (0 = host share, max 16)")
+    p.add_argument("--cpu-max-chunks", type=int, default=1024)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    return p.parse_args(argv)
+
+
+def host_threads() -> int:
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))  # the GPU box grants 16 host cores per GPU
+
+
+def load_traffic(kernel: str, workload_key: str):
+    """Per-launch HBM bytes of `kernel` measured by rocprofv3 --pmc (tools/pmc_traffic.py)."""
+    best = None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json"))):
+        try:
+            d = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if d.get("kernel") == kernel and d.get("workload_key") == workload_key:
+            best = d
+    return None if best is None else float(best["bytes_per_launch"])
+
+
+def cpu_baseline(batch, data, n_chunks: int, chunk: int, threads: int, do_crc: bool):
+    """The oracle (C restatement of sha1.go block + crc32.go slicingUpdate) over the same chunks."""
+    import numpy as np
+
+    from oracle import oracle
+
+    oracle.build()
+    m = max(1, min(n_chunks, threads * max(1, n_chunks // threads)))
+    host = data[: m * chunk].cpu().numpy()
+    lens = np.full(m, chunk, dtype=np.uint64)
+    secs, sha, crc = oracle.hash_many(host, chunk, lens, threads)
+    got = batch.sha1_hex()[:m]
+    ok = got == [bytes(r).hex() for r in sha]
+    if do_crc:
+        ok = ok and bool((batch.crc_sum()[:m] == crc).all())
+    return {
+        "value": round(m * chunk / secs / GiB, 3),
+        "unit": "GiB/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{m} x {chunk >> 20} MiB chunks (fused SHA-1+CRC32 per filereceiver.go:208 MultiWriter order),"
+                  f" one chunk per thread at a time, {secs:.2f} s",
+        "digests_match_gpu": bool(ok),
+    }
+
+
+def main(argv=None):
+    args = parse_args(argv)
+    import numpy as np
+    import torch
+
+    from efes_amd import MODE_AUTO, MODE_DEEP, MODE_WIDE
+    from efes_amd.batch import DeviceBatch
+    from efes_amd.hashing import default_context
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = f"cuda:{local}"
+    torch.cuda.set_device(local)
+    ctx = default_context(local)
+    stream = torch.cuda.Stream(device=device)
+    mode = {"auto": MODE_AUTO, "deep": MODE_DEEP, "wide": MODE_WIDE}[args.mode]
+
+    n, chunk = args.chunks, args.chunk_bytes
+    nbytes = n * chunk
+    with torch.cuda.stream(stream):
+        data = torch.empty(nbytes, dtype=torch.uint8, device=device)
+        ctx.fill_synthetic(data.data_ptr(), nbytes, 0xEFE5 ^ (rank << 32), stream.cuda_stream)
+        batch = DeviceBatch(data.data_ptr(), np.arange(n, dtype=np.uint64) * chunk, np.full(n, chunk),
+                            sha1=True, crc32=not args.sha1_only, finalize=True, fresh=True, ctx=ctx,
+                            device=device)
+        for _ in range(args.warmup):
+            batch.submit(mode)
+        torch.cuda.synchronize(device)
+        assert (batch.status_host() == 0).all(), "hash jobs reported an error status"
+
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize(device)
+        t0 = time.perf_counter()
+        ev0.record(stream)
+        for _ in range(args.steps):
+            batch.submit(mode)
+        ev1.record(stream)
+        torch.cuda.synchronize(device)
+        if dist:
+            dist.barrier()
+        wall = time.perf_counter() - t0
+    kernel_ms = ev0.elapsed_time(ev1) / max(1, args.steps)
+
+    if dist:
+        t = torch.tensor([wall], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall = float(t.item())
+
+    total_bytes = world * nbytes * args.steps
+    value = total_bytes / wall / GiB
+    kernel_name = "deep_kernel" if (mode == MODE_DEEP or (mode == MODE_AUTO and n <= 1536)) else "wide_kernel"
+    workload_key = f"{n}x{chunk}:{'sha1' if args.sha1_only else 'sha1+crc32'}"
+    achieved = nbytes / (kernel_ms * 1e-3) / 1e9
+    traffic = load_traffic(kernel_name, workload_key)
+    out = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(wall * 1e3 / args.steps, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic (device-generated splitmix64 bytes)",
+        "config": {
+            "workload": ("1024 x 4 MiB chunks, SHA-1 only (BASELINE configs[1])" if args.sha1_only else
+                         "1024 x 4 MiB chunks, fused single-pass SHA-1 + CRC32 (BASELINE configs[2])")
+            if (n, chunk) == (1024, 4 << 20) else f"{n} x {chunk} B chunks",
+            "chunks_per_gpu": n,
+            "chunk_bytes": chunk,
+            "kernel": kernel_name,
+            "parallelism": f"per-GPU queues x{world}, no collectives",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 2),
+            "peak": HBM_PEAK_GBPS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBPS, 5),
+            "traffic": traffic,
+            "kernel_ms": round(kernel_ms, 4),
+            "algorithmic_bytes_per_launch": nbytes,
+        },
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        threads = args.cpu_threads or host_threads()
+        out["cpu_baseline"] = cpu_baseline(batch, data, min(n, args.cpu_max_chunks), chunk, threads, not args.sha1_only)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

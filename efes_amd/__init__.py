@@ -7,7 +7,7 @@ efes_amd/csrc/).  This package is its Python host layer:
   efes_amd.batch   -- device-resident batches of independent jobs (the hot path).
 """
 from ._lib import (EFES_ERR_ARG, EFES_ERR_DEVICE_FAULT, EFES_ERR_HIP, EFES_ERR_INVALID_DIGEST,  # noqa: F401
-                   EFES_ERR_NO_DEVICE, EFES_ERR_NOMEM, EFES_ERR_STATE, EFES_JOB_FINALIZE, EFES_OK, MODE_AUTO,
+                   EFES_ERR_NO_DEVICE, EFES_ERR_NOMEM, EFES_ERR_STATE, EFES_JOB_FINALIZE, EFES_JOB_INIT, EFES_OK, MODE_AUTO,
                    MODE_DEEP, MODE_WIDE, EfesError, lib)
 
 __version__ = "0.1.0"

@@ -13,6 +13,9 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libefeshash.so")
+# Developer override for the range-checked debug build (tools/debug_checked.py); never set in production.
+if os.environ.get("EFES_LIB_OVERRIDE"):
+    LIB_PATH = os.environ["EFES_LIB_OVERRIDE"]
 
 EFES_OK = 0
 EFES_ERR_INVALID_DIGEST = -1
@@ -24,6 +27,7 @@ EFES_ERR_NOMEM = -6
 EFES_ERR_DEVICE_FAULT = -7
 
 EFES_JOB_FINALIZE = 0x1
+EFES_JOB_INIT = 0x2
 MODE_AUTO, MODE_DEEP, MODE_WIDE = 0, 1, 2
 
 
@@ -109,10 +113,28 @@ class EfesError(RuntimeError):
 _lib = None
 
 
+def _bind_process_hip_runtime() -> None:
+    """Make the process use ONE HIP runtime.
+
+    torch ships its own libamdhip64 (SONAME libamdhip64.so.7, ROCm 7.0); libefeshash.so
+    needs libamdhip64.so.7 and would otherwise pull /opt/rocm's (7.2) through its RUNPATH.
+    Two runtimes in one process do not share devices (torch then reports "No HIP GPUs").
+    Importing torch first lets the dynamic linker satisfy our NEEDED entry with torch's
+    already-loaded runtime.  EFES_NO_TORCH=1 skips this (pure-HIP hosts).
+    """
+    if os.environ.get("EFES_NO_TORCH") == "1":
+        return
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def lib() -> ctypes.CDLL:
     """Load libefeshash.so (raises if it has not been built -- no fallback path exists)."""
     global _lib
     if _lib is None:
+        _bind_process_hip_runtime()
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"{LIB_PATH} not built; run __graft_entry__.build() or python -m efes_amd.build")
         L = ctypes.CDLL(LIB_PATH)

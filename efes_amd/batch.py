@@ -9,7 +9,7 @@ from __future__ import annotations
 
 import numpy as np
 
-from ._lib import EFES_JOB_FINALIZE, JOB_DTYPE, MODE_AUTO, SHA1_STATE_DTYPE
+from ._lib import EFES_JOB_FINALIZE, EFES_JOB_INIT, JOB_DTYPE, MODE_AUTO, SHA1_STATE_DTYPE
 from .hashing import Context, default_context
 
 IV = np.array([0x67452301, 0xEFCDAB89, 0x98BADCFE, 0x10325476, 0xC3D2E1F0], dtype=np.uint32)
@@ -23,10 +23,15 @@ def fresh_states(n: int) -> np.ndarray:
 
 
 class DeviceBatch:
-    """Jobs j = 0..N-1: Write(data[offsets[j] : offsets[j]+lengths[j]]) into state j (+ Sum)."""
+    """Jobs j = 0..N-1: Write(data[offsets[j] : offsets[j]+lengths[j]]) into state j (+ Sum).
+
+    Kernels run on torch's current stream when it is not the null stream; a null-stream
+    handle (0) selects the context's own stream (efes_hash.h), and run() synchronises the
+    whole device either way.
+    """
 
     def __init__(self, data_ptr: int, offsets, lengths, *, sha1: bool = True, crc32: bool = True,
-                 finalize: bool = True, states: np.ndarray | None = None, crcs: np.ndarray | None = None,
+                 finalize: bool = True, fresh: bool = False, states: np.ndarray | None = None, crcs: np.ndarray | None = None,
                  ctx: Context | None = None, device: str = "cuda:0"):
         import torch
 
@@ -54,7 +59,9 @@ class DeviceBatch:
             jobs["crc32"] = np.uint64(self.crcs.data_ptr()) + np.arange(n, dtype=np.uint64) * np.uint64(4)
         if finalize:
             jobs["sum"] = np.uint64(self.sums.data_ptr()) + np.arange(n, dtype=np.uint64) * np.uint64(24)
-            jobs["flags"] = EFES_JOB_FINALIZE
+            jobs["flags"] |= EFES_JOB_FINALIZE
+        if fresh:  # new chunks: start from NewSha1()/NewCRC32IEEE(), in-states are not read
+            jobs["flags"] |= EFES_JOB_INIT
         jobs["status"] = np.uint64(self.status.data_ptr()) + np.arange(n, dtype=np.uint64) * np.uint64(4)
         self.jobs_host = jobs
         self.jobs = torch.from_numpy(jobs.view(np.uint8).copy()).to(device)

@@ -24,6 +24,21 @@
 #include "efes_internal.hpp"
 #include "sha1_device.hpp"
 
+#ifdef EFES_CHECKED
+// Debug build only (tools/debug_checked.py): every data load is range-checked against the
+// job's [p, p+plen); a violation is printed and redirected to p so the kernel cannot fault.
+#include <stdio.h>
+#define EFES_RANGE(ptr, nbytes, lo, len, tag)                                                               \
+  (((const uint8_t*)(ptr) < (const uint8_t*)(lo) ||                                                          \
+    (const uint8_t*)(ptr) + (nbytes) > (const uint8_t*)(lo) + (len))                                         \
+       ? (printf("EFES_CHECKED %s: ptr=%p n=%d lo=%p len=%llu blk=%d thr=%d\n", tag, (const void*)(ptr),        \
+                 (int)(nbytes), (const void*)(lo), (unsigned long long)(len), (int)blockIdx.x, (int)threadIdx.x), \
+          (decltype(ptr))(lo))                                                                              \
+       : (ptr))
+#else
+#define EFES_RANGE(ptr, nbytes, lo, len, tag) (ptr)
+#endif
+
 namespace efes {
 
 // ------------------------------------------------------------------ CRC-32 helpers
@@ -48,10 +63,11 @@ __device__ __forceinline__ uint32_t crc_words_raw(const uint32_t (&t)[8][256], u
   return crc;
 }
 
-__device__ __forceinline__ uint32_t uniform32(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+// __builtin_amdgcn_readfirstlane returns int: go through uint32_t so the low half of a
+// 64-bit value is zero-extended (a sign-extended low half corrupts pointers >= 2^31).
+__device__ __forceinline__ uint32_t uniform32(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 __device__ __forceinline__ uint64_t uniform64(uint64_t v) {
-  return (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)v) |
-         ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32);
+  return (uint64_t)uniform32((uint32_t)v) | ((uint64_t)uniform32((uint32_t)(v >> 32)) << 32);
 }
 
 // Orders this wave's LDS stores before its later LDS loads from other lanes.
@@ -127,7 +143,7 @@ __device__ void deep_bulk(DeepLDS& L, int wave, int lane, const uint8_t* q, uint
     const int bi = lane - (64 - nb);
 #pragma unroll
     for (int k = 0; k < 16; ++k) le[k] = 0;
-    if (bi >= 0) load_block_le<kAligned16>(q + 64 * (uint64_t)bi, le);
+    if (bi >= 0) load_block_le<kAligned16>(EFES_RANGE(q + 64 * (uint64_t)bi, 64, q, 64 * nbulk, "deep-bulk0"), le);
   }
   while (b0 < nbulk) {
     const int off = 64 - nb;
@@ -165,7 +181,7 @@ __device__ void deep_bulk(DeepLDS& L, int wave, int lane, const uint8_t* q, uint
       const int bj = lane - (64 - nb1);
 #pragma unroll
       for (int k = 0; k < 16; ++k) le[k] = 0;
-      if (bj >= 0) load_block_le<kAligned16>(q + 64 * (b1 + (uint64_t)bj), le);
+      if (bj >= 0) load_block_le<kAligned16>(EFES_RANGE(q + 64 * (b1 + (uint64_t)bj), 64, q, 64 * nbulk, "deep-bulk1"), le);
     }
     if (do_sha) {
       wave_lds_sync();
@@ -186,14 +202,18 @@ __device__ void deep_job(DeepLDS& L, int wave, int lane, const DeepJob& J) {
   uint32_t h[5] = {0, 0, 0, 0, 0};
   int64_t nx = 0;
   uint64_t len = 0;
-  if (do_sha) {
+  const bool init = (J.flags & EFES_JOB_INIT) != 0;
+  if (do_sha && init) {  // NewSha1(): zero value + Reset (sha1.go:36-52)
+    h[0] = kIV0; h[1] = kIV1; h[2] = kIV2; h[3] = kIV3; h[4] = kIV4;
+    if (lane < 16) reinterpret_cast<uint32_t*>(xs)[lane] = 0u;
+  } else if (do_sha) {
 #pragma unroll
     for (int k = 0; k < 5; ++k) h[k] = uniform32(J.st->h[k]);
     nx = (int64_t)uniform64((uint64_t)J.st->nx);
     len = uniform64(J.st->len);
     if (lane < 16) reinterpret_cast<uint32_t*>(xs)[lane] = reinterpret_cast<const uint32_t*>(J.st->x)[lane];
   }
-  uint32_t crc_raw = do_crc ? ~uniform32(J.cs->crc) : 0u;
+  uint32_t crc_raw = do_crc ? (init ? 0xFFFFFFFFu : ~uniform32(J.cs->crc)) : 0u;
 
   if (do_sha && nx > 64) {  // Go: copy(d.x[d.nx:], p) panics (sha1.go:62)
     if (lane == 0 && J.status) *J.status = EFES_ERR_STATE;
@@ -209,7 +229,7 @@ __device__ void deep_job(DeepLDS& L, int wave, int lane, const DeepJob& J) {
   if (do_sha && nx > 0) {
     const uint32_t room = (uint32_t)(64 - nx);
     const uint32_t nh = plen < room ? (uint32_t)plen : room;
-    if ((uint32_t)lane < nh) xs[nx + lane] = p[lane];
+    if ((uint32_t)lane < nh) xs[nx + lane] = *EFES_RANGE(p + lane, 1, p, plen, "deep-head");
     wave_lds_sync();
     if ((uint32_t)nx + nh == 64) {
       uint32_t w[16];
@@ -223,7 +243,7 @@ __device__ void deep_job(DeepLDS& L, int wave, int lane, const DeepJob& J) {
     pos = nh;
   }
   if (do_crc)
-    for (uint64_t i = 0; i < pos; ++i) crc_raw = crc_byte(L.tab.slice8[0], crc_raw, p[i]);
+    for (uint64_t i = 0; i < pos; ++i) crc_raw = crc_byte(L.tab.slice8[0], crc_raw, *EFES_RANGE(p + i, 1, p, plen, "deep-crchead"));
 
   // ---- bulk whole blocks (sha1.go:70-74)
   const uint8_t* q = p + pos;
@@ -239,9 +259,9 @@ __device__ void deep_job(DeepLDS& L, int wave, int lane, const DeepJob& J) {
   const uint64_t tpos = pos + (nbulk << 6);
   const uint32_t r = (uint32_t)(plen - tpos);
   if (do_crc)
-    for (uint32_t i = 0; i < r; ++i) crc_raw = crc_byte(L.tab.slice8[0], crc_raw, p[tpos + i]);
+    for (uint32_t i = 0; i < r; ++i) crc_raw = crc_byte(L.tab.slice8[0], crc_raw, *EFES_RANGE(p + tpos + i, 1, p, plen, "deep-crctail"));
   if (do_sha && r > 0) {
-    if ((uint32_t)lane < r) xs[lane] = p[tpos + lane];
+    if ((uint32_t)lane < r) xs[lane] = *EFES_RANGE(p + tpos + lane, 1, p, plen, "deep-tail");
     nx_new = r;
   }
   wave_lds_sync();
@@ -334,6 +354,11 @@ __global__ __launch_bounds__(64 * kDeepWaves, 1) void deep_kernel(const efes_job
   J.sum = reinterpret_cast<uint8_t*>(uniform64(reinterpret_cast<uint64_t>(jb->sum)));
   J.status = reinterpret_cast<int32_t*>(uniform64(reinterpret_cast<uint64_t>(jb->status)));
   J.flags = uniform32(jb->flags);
+#ifdef EFES_CHECKED
+  if (lane == 0)
+    printf("EFES_CHECKED job %u p=%p len=%llu st=%p cs=%p sum=%p status=%p flags=%u\n", j, (const void*)J.p,
+           (unsigned long long)J.plen, (void*)J.st, (void*)J.cs, (void*)J.sum, (void*)J.status, J.flags);
+#endif
   deep_job(L, wave, lane, J);
 }
 
@@ -380,7 +405,12 @@ __global__ __launch_bounds__(64 * kWideWaves, 2) void wide_kernel(const efes_job
   uint32_t h[5] = {0, 0, 0, 0, 0};
   int64_t nx = 0;
   uint64_t len = 0;
-  if (do_sha) {
+  const bool init = live && (jb.flags & EFES_JOB_INIT) != 0;
+  if (do_sha && init) {  // NewSha1() (sha1.go:36-52)
+    h[0] = kIV0; h[1] = kIV1; h[2] = kIV2; h[3] = kIV3; h[4] = kIV4;
+#pragma unroll
+    for (int k = 0; k < 64; ++k) xl[k] = 0;
+  } else if (do_sha) {
 #pragma unroll
     for (int k = 0; k < 5; ++k) h[k] = st->h[k];
     nx = st->nx;
@@ -391,7 +421,7 @@ __global__ __launch_bounds__(64 * kWideWaves, 2) void wide_kernel(const efes_job
       xl[4 * k] = (uint8_t)v; xl[4 * k + 1] = (uint8_t)(v >> 8); xl[4 * k + 2] = (uint8_t)(v >> 16); xl[4 * k + 3] = (uint8_t)(v >> 24);
     }
   }
-  uint32_t crc_raw = do_crc ? ~cs->crc : 0u;
+  uint32_t crc_raw = do_crc ? (init ? 0xFFFFFFFFu : ~cs->crc) : 0u;
   const bool bad = do_sha && nx > 64;  // sha1.go:62 panic
   const bool go = live && !bad;
 

@@ -79,6 +79,8 @@ void* efes_ctx_stream(efes_ctx* ctx);
 
 /* ---- layer 1: batched device-resident jobs ----------------------------------------- */
 #define EFES_JOB_FINALIZE 0x1u /* also write Sum of the post-Write state to `sum` */
+#define EFES_JOB_INIT 0x2u     /* start from NewSha1() / NewCRC32IEEE() (sha1.go:48-52, crc32.go:68):
+                                  the in-states are not read, only written (a fresh chunk) */
 
 /* One `Write(p)` (+ optional Sum) of len(p) = length bytes at device address `data`.
  * sha1 / crc32: device states updated in place; either may be NULL to skip that hash

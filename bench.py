@@ -48,6 +48,10 @@ def parse_args(argv=None):
     p.add_argument("--cpu-threads", type=int, default=0, help="cpu_baseline threads (0 = host share, max 16)")
     p.add_argument("--cpu-max-chunks", type=int, default=1024)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--host-inclusive", choices=["auto", "on", "off"], default="auto",
+                   help="also time the host-resident path (pinned H2D + hash); auto = N=1 only")
+    p.add_argument("--segment-bytes", type=int, default=1 << 20, help="host-inclusive pipeline segment")
+    p.add_argument("--cpu-seconds", type=float, default=10.0, help="minimum CPU work in the cpu_baseline sample")
     return p.parse_args(argv)
 
 
@@ -72,7 +76,7 @@ def load_traffic(kernel: str, workload_key: str):
     return None if best is None else float(best["bytes_per_launch"])
 
 
-def cpu_baseline(batch, data, n_chunks: int, chunk: int, threads: int, do_crc: bool):
+def cpu_baseline(batch, data, n_chunks: int, chunk: int, threads: int, do_crc: bool, min_seconds: float = 10.0):
     """The oracle (C restatement of sha1.go block + crc32.go slicingUpdate) over the same chunks."""
     import numpy as np
 
@@ -82,20 +86,43 @@ def cpu_baseline(batch, data, n_chunks: int, chunk: int, threads: int, do_crc: b
     m = max(1, min(n_chunks, threads * max(1, n_chunks // threads)))
     host = data[: m * chunk].cpu().numpy()
     lens = np.full(m, chunk, dtype=np.uint64)
-    secs, sha, crc = oracle.hash_many(host, chunk, lens, threads)
+    secs, reps = 0.0, 0
+    while secs < min_seconds or reps == 0:  # a bounded sample of >= min_seconds of CPU work
+        dt, sha, crc = oracle.hash_many(host, chunk, lens, threads)
+        secs += dt
+        reps += 1
     got = batch.sha1_hex()[:m]
     ok = got == [bytes(r).hex() for r in sha]
     if do_crc:
         ok = ok and bool((batch.crc_sum()[:m] == crc).all())
     return {
-        "value": round(m * chunk / secs / GiB, 3),
+        "value": round(reps * m * chunk / secs / GiB, 3),
         "unit": "GiB/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{m} x {chunk >> 20} MiB chunks (fused SHA-1+CRC32 per filereceiver.go:208 MultiWriter order),"
-                  f" one chunk per thread at a time, {secs:.2f} s",
+        "sample": f"{reps} pass(es) over {m} x {chunk >> 20} MiB chunks of the same workload (fused SHA-1+CRC32 in"
+                  f" filereceiver.go:208 MultiWriter order), one chunk per thread at a time, {secs:.1f} s",
         "digests_match_gpu": bool(ok),
     }
+
+
+def host_inclusive(ctx, data, n: int, chunk: int, do_crc: bool, segment: int, batch):
+    """The same chunks starting in pinned host memory: H2D copies overlapped with hashing."""
+    from efes_amd.batch import HostBatch, PinnedHostBuffer
+
+    buf = PinnedHostBuffer(n * chunk, ctx)
+    try:
+        ctx.copy_to_host(buf.ptr, data.data_ptr(), n * chunk)
+        hb = HostBatch(buf.ptr, [i * chunk for i in range(n)], [chunk] * n, crc32=do_crc, ctx=ctx)
+        hb.run(segment)  # warm-up (first-touch of the pipeline buffers)
+        hb = HostBatch(buf.ptr, [i * chunk for i in range(n)], [chunk] * n, crc32=do_crc, ctx=ctx)
+        st = hb.run(segment)
+        ok = hb.sha1_hex() == batch.sha1_hex() and (not do_crc or bool((hb.crc_sum() == batch.crc_sum()).all()))
+    finally:
+        buf.free()
+    return {"value": round(st.bytes / st.seconds / GiB, 3), "unit": "GiB/s", "segment_bytes": segment,
+            "segments": st.segments, "digests_match_device_path": bool(ok),
+            "note": "pinned host chunks -> hipMemcpyAsync H2D (copy stream) overlapped with hashing; not `value`"}
 
 
 def main(argv=None):
@@ -197,9 +224,12 @@ def main(argv=None):
         },
         "cpu_baseline": None,
     }
+    if args.host_inclusive == "on" or (args.host_inclusive == "auto" and world == 1):
+        out["host_inclusive"] = host_inclusive(ctx, data, n, chunk, not args.sha1_only, args.segment_bytes, batch)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = args.cpu_threads or host_threads()
-        out["cpu_baseline"] = cpu_baseline(batch, data, min(n, args.cpu_max_chunks), chunk, threads, not args.sha1_only)
+        out["cpu_baseline"] = cpu_baseline(batch, data, min(n, args.cpu_max_chunks), chunk, threads, not args.sha1_only,
+                                           args.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:

@@ -31,6 +31,11 @@ EFES_JOB_INIT = 0x2
 MODE_AUTO, MODE_DEEP, MODE_WIDE = 0, 1, 2
 
 
+class HostStats(ctypes.Structure):
+    _fields_ = [("seconds", ctypes.c_double), ("bytes", ctypes.c_uint64), ("segments", ctypes.c_uint32),
+                ("_reserved", ctypes.c_uint32)]
+
+
 class Sha1State(ctypes.Structure):
     """efes_sha1_state == sha1.go:29-34 sha1digest (+4 pad bytes)."""
     _fields_ = [("h", ctypes.c_uint32 * 5), ("x", ctypes.c_uint8 * 64), ("_pad", ctypes.c_uint32),
@@ -74,6 +79,9 @@ SIGNATURES = {
     "efes_copy_to_device": (_I, [_VP, _VP, _VP, _S, _VP]),
     "efes_copy_to_host": (_I, [_VP, _VP, _VP, _S, _VP]),
     "efes_fill_synthetic": (_I, [_VP, _VP, _S, _U64, _VP]),
+    "efes_hash_host": (_I, [_VP, _VP, _U32, _U64, _P(HostStats)]),
+    "efes_host_alloc": (_I, [_VP, _S, _P(_VP)]),
+    "efes_host_free": (_I, [_VP, _VP]),
     "efes_sha1_new": (_I, [_VP, _P(_VP)]),
     "efes_sha1_new_zero": (_I, [_VP, _P(_VP)]),
     "efes_sha1_free": (None, [_VP]),

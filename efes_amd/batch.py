@@ -99,3 +99,86 @@ class DeviceBatch:
 
     def states_host(self) -> np.ndarray:
         return self.states.cpu().numpy().view(SHA1_STATE_DTYPE)[: self.n]
+
+
+class PinnedHostBuffer:
+    """Pinned host memory from efes_host_alloc (a socket-buffer pool registered for DMA)."""
+
+    def __init__(self, nbytes: int, ctx: Context | None = None):
+        import ctypes
+
+        from ._lib import check, lib
+
+        self.ctx = ctx or default_context()
+        p = ctypes.c_void_p()
+        check(lib().efes_host_alloc(self.ctx.handle, nbytes, ctypes.byref(p)), "efes_host_alloc")
+        self.ptr = p.value
+        self.nbytes = nbytes
+        self.array = np.ctypeslib.as_array((ctypes.c_uint8 * max(nbytes, 1)).from_address(self.ptr))[:nbytes]
+
+    def free(self) -> None:
+        from ._lib import lib
+
+        if self.ptr:
+            self.array = None
+            lib().efes_host_free(self.ctx.handle, self.ptr)
+            self.ptr = None
+
+    def __del__(self):  # pragma: no cover - interpreter teardown order
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class HostBatch:
+    """Jobs whose bytes, states and sums live in HOST memory (efes_hash_host).
+
+    Message j = host bytes [data_ptr + offsets[j], + lengths[j]); each is copied to HBM in
+    `segment_bytes` pieces on a copy stream while the previous piece hashes (the per-PATCH
+    resume of filereceiver.go:182-226, with the state kept on the device).
+    """
+
+    def __init__(self, data_ptr: int, offsets, lengths, *, sha1: bool = True, crc32: bool = True,
+                 finalize: bool = True, fresh: bool = True, states: np.ndarray | None = None,
+                 crcs: np.ndarray | None = None, ctx: Context | None = None):
+        self.ctx = ctx or default_context()
+        offsets = np.asarray(offsets, dtype=np.uint64)
+        lengths = np.asarray(lengths, dtype=np.uint64)
+        n = self.n = int(offsets.size)
+        self.states = fresh_states(n) if states is None else np.array(states, dtype=SHA1_STATE_DTYPE)
+        self.crcs = np.zeros(n, np.uint32) if crcs is None else np.array(crcs, dtype=np.uint32)
+        self.sums = np.zeros((max(n, 1), 24), np.uint8)
+        self.status = np.full(max(n, 1), -99, np.int32)
+        jobs = np.zeros(n, dtype=JOB_DTYPE)
+        jobs["data"] = np.uint64(data_ptr) + offsets
+        jobs["length"] = lengths
+        idx = np.arange(n, dtype=np.uint64)
+        if sha1:
+            jobs["sha1"] = np.uint64(self.states.ctypes.data) + idx * np.uint64(SHA1_STATE_DTYPE.itemsize)
+        if crc32:
+            jobs["crc32"] = np.uint64(self.crcs.ctypes.data) + idx * np.uint64(4)
+        if finalize:
+            jobs["sum"] = np.uint64(self.sums.ctypes.data) + idx * np.uint64(24)
+            jobs["flags"] |= EFES_JOB_FINALIZE
+        if fresh:
+            jobs["flags"] |= EFES_JOB_INIT
+        jobs["status"] = np.uint64(self.status.ctypes.data) + idx * np.uint64(4)
+        self.jobs = jobs
+
+    def run(self, segment_bytes: int = 1 << 20):
+        """Returns efes_host_stats (seconds, bytes, segments) of the copy+hash pipeline."""
+        import ctypes
+
+        from ._lib import HostStats, check, lib
+
+        st = HostStats()
+        check(lib().efes_hash_host(self.ctx.handle, self.jobs.ctypes.data, self.n, segment_bytes,
+                                   ctypes.byref(st)), "efes_hash_host")
+        return st
+
+    def sha1_hex(self) -> list[str]:
+        return [bytes(r[:20]).hex() for r in self.sums[: self.n]]
+
+    def crc_sum(self) -> np.ndarray:
+        return self.crcs[: self.n]

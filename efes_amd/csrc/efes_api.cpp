@@ -21,12 +21,6 @@
 
 using efes::Tables;
 
-struct efes_ctx {
-  int device = 0;
-  hipStream_t stream = nullptr;
-  Tables* d_tabs = nullptr;
-  std::mutex mu;
-};
 
 namespace {
 
@@ -34,17 +28,7 @@ constexpr size_t kFlushBytes = 64u << 20;
 
 int hip_err(hipError_t e) { return e == hipSuccess ? EFES_OK : EFES_ERR_HIP; }
 
-struct DeviceGuard {
-  int prev = -1;
-  explicit DeviceGuard(int dev) {
-    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-    if (prev != dev) (void)hipSetDevice(dev);
-  }
-  ~DeviceGuard() {
-    int cur = -1;
-    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
-  }
-};
+using efes::DeviceGuard;
 
 hipStream_t pick(efes_ctx* ctx, void* s) { return s ? static_cast<hipStream_t>(s) : ctx->stream; }
 

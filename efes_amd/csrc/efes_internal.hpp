@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <mutex>
+
 #include "../../include/efes_hash.h"
 
 namespace efes {
@@ -29,4 +31,26 @@ hipError_t launch_fill(void* dst, size_t bytes, uint64_t seed, hipStream_t s);
 constexpr int kDeepWaves = 4;  // waves per DEEP workgroup: one per SIMD
 constexpr uint32_t kAutoDeepMaxJobs = 1536;  // AUTO: DEEP up to ~1.5 waves per SIMD
 
+// Makes `dev` current for the scope and restores the caller's device (C ABI calls may come
+// from any host thread, efes_hash.h).
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
 }  // namespace efes
+
+// One GPU: its CRC tables in HBM and its own stream (efes_ctx_create).
+struct efes_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  efes::Tables* d_tabs = nullptr;
+  std::mutex mu;
+};

@@ -50,6 +50,12 @@ class Context:
         check(lib().efes_fill_synthetic(self.handle, ptr, nbytes, seed & 0xFFFFFFFFFFFFFFFF, stream),
               "efes_fill_synthetic")
 
+    def copy_to_host(self, dst_host: int, src_device: int, nbytes: int, stream: int | None = None) -> None:
+        check(lib().efes_copy_to_host(self.handle, dst_host, src_device, nbytes, stream), "efes_copy_to_host")
+
+    def copy_to_device(self, dst_device: int, src_host: int, nbytes: int, stream: int | None = None) -> None:
+        check(lib().efes_copy_to_device(self.handle, dst_device, src_host, nbytes, stream), "efes_copy_to_device")
+
     def close(self) -> None:
         if self.handle:
             lib().efes_ctx_destroy(self.handle)

@@ -120,6 +120,28 @@ int efes_copy_to_host(efes_ctx* ctx, void* dst_host, const void* src_device, siz
 /* Synthetic benchmark bytes: little-endian splitmix64 stream, z_i = mix(seed + (i+1)*0x9E3779B97F4A7C15). */
 int efes_fill_synthetic(efes_ctx* ctx, void* dst_device, size_t bytes, uint64_t seed, void* stream);
 
+/* ---- host-resident ingest -------------------------------------------------------------
+ * The reference's path starts in host memory (a socket buffer, filereceiver.go:208-209).
+ * efes_hash_host runs the jobs of a HOST array whose data/sha1/crc32/sum/status pointers are
+ * all HOST memory: segment s (segment_bytes, rounded up to 64; 0 = 1 MiB) of every message is
+ * copied H2D with hipMemcpyAsync on a copy stream into one of two device slots while segment
+ * s-1 is hashed on the context stream; states stay on the device between segments (the
+ * per-PATCH resume of filereceiver.go:182-226); states, sums and status are copied back at
+ * the end.  Messages whose host addresses advance by a constant stride are copied with one
+ * 2D copy per segment.  For the full PCIe rate the data should be pinned (efes_host_alloc).
+ * Synchronous; stats (may be NULL) time the pipeline from the first copy to the last result. */
+typedef struct efes_host_stats {
+    double seconds;    /* wall time of the copy+hash pipeline */
+    uint64_t bytes;    /* message bytes moved and hashed */
+    uint32_t segments; /* pipeline steps */
+    uint32_t _reserved;
+} efes_host_stats;
+
+int efes_hash_host(efes_ctx* ctx, const efes_job* jobs_host, uint32_t njobs, uint64_t segment_bytes,
+                   efes_host_stats* stats);
+int efes_host_alloc(efes_ctx* ctx, size_t bytes, void** out); /* pinned host memory (hipHostMalloc) */
+int efes_host_free(efes_ctx* ctx, void* p);
+
 /* ---- layer 2: streaming digests mirroring the Go surface ---------------------------- */
 typedef struct efes_sha1 efes_sha1;
 typedef struct efes_crc32 efes_crc32;

@@ -404,3 +404,51 @@ def test_large_streaming_write_flushes(env):
     for i in range(0, len(data), 32 * 1024):  # io.Copy granularity
         d.write(data[i:i + 32 * 1024])
     assert d.sum().hex() == hashlib.sha1(data).hexdigest()
+
+
+# ---------------------------------------------------------------- host-resident ingest (efes_hash_host)
+
+@pytest.mark.parametrize("segment", [64, 4096, 1 << 20])
+def test_host_ingest_matches_oracle(env, oracle, segment):
+    """Bytes start in host memory (filereceiver.go:208-209 reads a socket): segmented H2D + hash."""
+    from efes_amd.batch import HostBatch
+    rng = random.Random(segment)
+    lengths = [0, 1, 63, 64, 65, 1000, 4096, 70001, 300000] + [rng.randint(0, 200000) for _ in range(23)]
+    offsets, pos = [], 0
+    for L in lengths:
+        offsets.append(pos)
+        pos += L + rng.randint(0, 9)
+    host = oracle.fill_synthetic(pos + 8, 77)  # ordinary (pageable) host memory
+    hb = HostBatch(host.ctypes.data, offsets, lengths, ctx=env["ctx"])
+    st = hb.run(segment)
+    assert st.bytes == sum(lengths)
+    assert (hb.status[: hb.n] == 0).all()
+    for i, (o, L) in enumerate(zip(offsets, lengths)):
+        d = host[o:o + L].tobytes()
+        assert hb.sha1_hex()[i] == hashlib.sha1(d).hexdigest(), (segment, L)
+        assert int(hb.crc_sum()[i]) == zlib.crc32(d), (segment, L)
+
+
+def test_host_ingest_pinned_strided_and_resume(env, oracle):
+    """Pinned, constant-stride batch (one 2D copy per segment) resumed from mid-stream states."""
+    from efes_amd.batch import HostBatch, PinnedHostBuffer
+    rng = random.Random(5)
+    n, stride, L = 40, 50000, 49999
+    buf = PinnedHostBuffer(n * stride, env["ctx"])
+    try:
+        buf.array[:] = oracle.fill_synthetic(n * stride, 8)
+        states, crcs = midstream_states(oracle, env, n, rng)
+        hb = HostBatch(buf.ptr, [i * stride for i in range(n)], [L] * n, fresh=False, states=states, crcs=crcs,
+                       ctx=env["ctx"])
+        hb.run(8192)
+        datas = [buf.array[i * stride:i * stride + L].tobytes() for i in range(n)]
+        for i, d in enumerate(datas):
+            e_status, e_state, e_crc, e_sum = oracle_expect(oracle, states[i], d, int(crcs[i]))
+            assert hb.status[i] == e_status
+            assert list(hb.states[i]["h"]) == e_state["h"] and int(hb.states[i]["nx"]) == e_state["nx"]
+            assert int(hb.states[i]["len"]) == e_state["len"] and bytes(hb.states[i]["x"]) == e_state["x"]
+            assert int(hb.crcs[i]) == e_crc
+            if e_sum is not None:
+                assert bytes(hb.sums[i][:20]) == e_sum
+    finally:
+        buf.free()

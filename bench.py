@@ -134,9 +134,9 @@ def main(argv=None):
     from efes_amd.batch import DeviceBatch
     from efes_amd.hashing import default_context
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    from efes_amd.shard import env_rank, max_over_ranks
+
+    rank, local, world = env_rank()
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
     dist = None
@@ -179,10 +179,7 @@ def main(argv=None):
         wall = time.perf_counter() - t0
     kernel_ms = ev0.elapsed_time(ev1) / max(1, args.steps)
 
-    if dist:
-        t = torch.tensor([wall], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        wall = float(t.item())
+    wall = max_over_ranks(wall, device)  # the job takes as long as its slowest rank
 
     total_bytes = world * nbytes * args.steps
     value = total_bytes / wall / GiB

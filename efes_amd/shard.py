@@ -1,0 +1,78 @@
+"""Multi-GPU placement of independent uploads: per-GPU work queues, no collectives on the data path.
+
+Objects (uploads) are independent units: each one's chunks must be hashed in order on ONE
+device because the SHA-1 state chains from chunk to chunk (filereceiver.go:182-226 resumes
+the `.info` state per PATCH).  So the unit of placement is the object, and a rank's queue is
+just a list of objects.  Placement is longest-processing-time-first (LPT) by byte count,
+which bounds the makespan by 4/3 of optimal and matters for config 4's 64 KiB..64 MiB mix
+(SURVEY.md §8(d)), where one long object sets the tail.
+
+The only cross-rank communication is for measurement (max-over-ranks wall time) and, in the
+tests, gathering digests to compare against a single-process run.
+"""
+from __future__ import annotations
+
+import heapq
+import os
+
+import numpy as np
+
+
+def lpt_assign(sizes, world: int) -> list[list[int]]:
+    """Object indices per rank: largest first onto the least-loaded rank (ties -> lower rank).
+
+    Deterministic, so every rank computes the same plan locally without communicating.
+    """
+    if world < 1:
+        raise ValueError("world must be >= 1")
+    sizes = np.asarray(sizes, dtype=np.int64)
+    order = np.argsort(-sizes, kind="stable")
+    heap = [(0, r) for r in range(world)]
+    out: list[list[int]] = [[] for _ in range(world)]
+    for i in order:
+        load, r = heapq.heappop(heap)
+        out[r].append(int(i))
+        heapq.heappush(heap, (load + int(sizes[i]), r))
+    for q in out:
+        q.sort()  # stable submission order within a rank
+    return out
+
+
+def loads(sizes, plan) -> list[int]:
+    sizes = np.asarray(sizes, dtype=np.int64)
+    return [int(sizes[q].sum()) if q else 0 for q in plan]
+
+
+def env_rank() -> tuple[int, int, int]:
+    """(rank, local_rank, world_size) from the torch.distributed.run environment (defaults 0, 0, 1)."""
+    return (int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0")),
+            int(os.environ.get("WORLD_SIZE", "1")))
+
+
+def max_over_ranks(value: float, device=None) -> float:
+    """Max of a per-rank scalar (the job's wall time is the slowest rank's)."""
+    import torch
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return float(value)
+    t = torch.tensor([float(value)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def gather_results(local: dict[int, tuple[str, int]]) -> dict[int, tuple[str, int]]:
+    """Union of every rank's {object index: (sha1 hex, crc32)} (tests / verification only)."""
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return dict(local)
+    parts: list = [None] * dist.get_world_size()
+    dist.all_gather_object(parts, local)
+    out: dict[int, tuple[str, int]] = {}
+    for p in parts:
+        dup = set(out) & set(p)
+        if dup:
+            raise RuntimeError(f"objects hashed on two ranks: {sorted(dup)[:5]}")
+        out.update(p)
+    return out

@@ -127,7 +127,8 @@ int efes_fill_synthetic(efes_ctx* ctx, void* dst_device, size_t bytes, uint64_t 
  * copied H2D with hipMemcpyAsync on a copy stream into one of two device slots while segment
  * s-1 is hashed on the context stream; states stay on the device between segments (the
  * per-PATCH resume of filereceiver.go:182-226); states, sums and status are copied back at
- * the end.  Messages whose host addresses advance by a constant stride are copied with one
+ * the end.  Equivalent to one Write per segment (so the stale bytes x[nx:64] are those of
+ * segment-sized Writes, sha1.go:75-77).  Messages whose host addresses advance by a constant stride are copied with one
  * 2D copy per segment.  For the full PCIe rate the data should be pinned (efes_host_alloc).
  * Synchronous; stats (may be NULL) time the pipeline from the first copy to the last result. */
 typedef struct efes_host_stats {

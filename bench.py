@@ -44,6 +44,13 @@ def parse_args(argv=None):
     p.add_argument("--chunks", type=int, default=1024, help="chunks per GPU")
     p.add_argument("--chunk-bytes", type=int, default=4 << 20)
     p.add_argument("--mode", choices=["auto", "deep", "wide"], default="auto")
+    p.add_argument("--workload", choices=["chunks4m", "mixed", "ingest"], default="chunks4m",
+                   help="chunks4m = BASELINE configs[1]/[2] (the metric); mixed = configs[3]; ingest = configs[4]")
+    p.add_argument("--pool-gib", type=int, default=64, help="device pool aliased by mixed/ingest chunks")
+    p.add_argument("--mixed-chunks", type=int, default=65536)
+    p.add_argument("--ingest-tib", type=float, default=10.0)
+    p.add_argument("--ingest-scale", type=float, default=1.0)
+    p.add_argument("--ingest-batch", type=int, default=65536)
     p.add_argument("--sha1-only", action="store_true", help="BASELINE configs[1] (no CRC-32)")
     p.add_argument("--cpu-threads", type=int, default=0, help="cpu_baseline threads (0 = host share, max 16)")
     p.add_argument("--cpu-max-chunks", type=int, default=1024)
@@ -125,15 +132,72 @@ def host_inclusive(ctx, data, n: int, chunk: int, do_crc: bool, segment: int, ba
             "note": "pinned host chunks -> hipMemcpyAsync H2D (copy stream) overlapped with hashing; not `value`"}
 
 
-def main(argv=None):
-    args = parse_args(argv)
+def make_workload(args, rank: int, world: int, ctx, device: str, stream):
+    """Device-resident inputs + the job batches of one workload.
+
+    chunks4m (default, BASELINE configs[2] / configs[1] with --sha1-only): n x 4 MiB chunks
+        packed in HBM, one batch, one launch per step.
+    mixed (configs[3]): --mixed-chunks chunks whose sizes are the eleven ChunkSize values
+        64K..64M (chunksize.go) drawn uniformly (log-uniform in bytes, seed 7 + rank); they
+        alias a --pool-gib device pool at seeded 256-B aligned offsets; jobs are submitted
+        longest first so each wave's 64 lanes carry equal lengths. One step = all chunks.
+    ingest (configs[4]): this GPU's share of --ingest-tib TiB of 4 MiB chunks on an 8-GPU node
+        (fixed per GPU: weak scaling), scaled by --ingest-scale, in launches of
+        --ingest-batch chunks aliasing the pool. One step = one launch.
+    Returns (data tensor, [DeviceBatch...], bytes per step list, config dict).
+    """
     import numpy as np
     import torch
 
-    from efes_amd import MODE_AUTO, MODE_DEEP, MODE_WIDE
     from efes_amd.batch import DeviceBatch
-    from efes_amd.hashing import default_context
+    from efes_amd.chunksize import MIXED_CLASSES
 
+    kw = dict(sha1=True, crc32=not args.sha1_only, finalize=True, fresh=True, ctx=ctx, device=device)
+    seed = 0xEFE5 ^ (rank << 32)
+    if args.workload == "chunks4m":
+        n, chunk = args.chunks, args.chunk_bytes
+        data = torch.empty(n * chunk, dtype=torch.uint8, device=device)
+        ctx.fill_synthetic(data.data_ptr(), n * chunk, seed, stream.cuda_stream)
+        b = DeviceBatch(data.data_ptr(), np.arange(n, dtype=np.uint64) * chunk, np.full(n, chunk), **kw)
+        name = (("1024 x 4 MiB chunks, SHA-1 only (BASELINE configs[1])" if args.sha1_only else
+                 "1024 x 4 MiB chunks, fused single-pass SHA-1 + CRC32 (BASELINE configs[2])")
+                if (n, chunk) == (1024, 4 << 20) else f"{n} x {chunk} B chunks")
+        return data, [b], [n * chunk], {"workload": name, "chunks_per_gpu": n, "chunk_bytes": chunk}
+    pool = args.pool_gib << 30
+    data = torch.empty(pool, dtype=torch.uint8, device=device)
+    ctx.fill_synthetic(data.data_ptr(), pool, seed, stream.cuda_stream)
+    if args.workload == "mixed":
+        rng = np.random.default_rng(7 + rank)
+        sizes = np.asarray(MIXED_CLASSES, dtype=np.uint64)[rng.integers(0, len(MIXED_CLASSES), args.mixed_chunks)]
+        sizes = np.sort(sizes)[::-1].copy()  # longest first: equal lengths per wave, LPT tail
+        offs = (rng.integers(0, (pool - sizes.astype(np.int64)) // 256 + 1) * 256).astype(np.uint64)
+        b = DeviceBatch(data.data_ptr(), offs, sizes, **kw)
+        total = int(sizes.sum())
+        return data, [b], [total], {"workload": f"mixed ChunkSize 64K..64M x {args.mixed_chunks} chunks "
+                                                "(BASELINE configs[3])", "chunks_per_gpu": args.mixed_chunks,
+                                    "bytes_per_gpu": total, "pool_bytes": pool}
+    chunk = 4 << 20
+    per_gpu = int(round(args.ingest_tib * (1 << 40) / chunk / 8 * args.ingest_scale))
+    slots = pool // chunk
+    batches, nbytes = [], []
+    for start in range(0, per_gpu, args.ingest_batch):
+        m = min(args.ingest_batch, per_gpu - start)
+        idx = (np.arange(start, start + m, dtype=np.uint64) + np.uint64(rank * 7919)) % np.uint64(slots)
+        batches.append(DeviceBatch(data.data_ptr(), idx * np.uint64(chunk), np.full(m, chunk), **kw))
+        nbytes.append(m * chunk)
+    return data, batches, nbytes, {"workload": f"{args.ingest_tib:g} TiB ingest over 8 GPUs, this GPU's share "
+                                               f"x{args.ingest_scale:g} (BASELINE configs[4])",
+                                   "chunks_per_gpu": per_gpu, "chunk_bytes": chunk, "pool_bytes": pool,
+                                   "launches": len(batches)}
+
+
+def main(argv=None):
+    args = parse_args(argv)
+    import torch
+
+    from efes_amd import MODE_AUTO, MODE_DEEP, MODE_WIDE
+    from efes_amd._lib import kAutoDeepMaxJobs
+    from efes_amd.hashing import default_context
     from efes_amd.shard import env_rank, max_over_ranks
 
     rank, local, world = env_rank()
@@ -151,18 +215,14 @@ def main(argv=None):
     stream = torch.cuda.Stream(device=device)
     mode = {"auto": MODE_AUTO, "deep": MODE_DEEP, "wide": MODE_WIDE}[args.mode]
 
-    n, chunk = args.chunks, args.chunk_bytes
-    nbytes = n * chunk
     with torch.cuda.stream(stream):
-        data = torch.empty(nbytes, dtype=torch.uint8, device=device)
-        ctx.fill_synthetic(data.data_ptr(), nbytes, 0xEFE5 ^ (rank << 32), stream.cuda_stream)
-        batch = DeviceBatch(data.data_ptr(), np.arange(n, dtype=np.uint64) * chunk, np.full(n, chunk),
-                            sha1=True, crc32=not args.sha1_only, finalize=True, fresh=True, ctx=ctx,
-                            device=device)
+        data, batches, step_bytes, config = make_workload(args, rank, world, ctx, device, stream)
+        steps = args.steps if len(batches) == 1 else len(batches)
         for _ in range(args.warmup):
-            batch.submit(mode)
+            batches[0].submit(mode)
         torch.cuda.synchronize(device)
-        assert (batch.status_host() == 0).all(), "hash jobs reported an error status"
+        if args.warmup:
+            assert (batches[0].status_host() == 0).all(), "hash jobs reported an error status"
 
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         if dist:
@@ -170,63 +230,64 @@ def main(argv=None):
         torch.cuda.synchronize(device)
         t0 = time.perf_counter()
         ev0.record(stream)
-        for _ in range(args.steps):
-            batch.submit(mode)
+        for k in range(steps):
+            batches[k % len(batches)].submit(mode)
         ev1.record(stream)
         torch.cuda.synchronize(device)
         if dist:
             dist.barrier()
         wall = time.perf_counter() - t0
-    kernel_ms = ev0.elapsed_time(ev1) / max(1, args.steps)
-
+    kernel_ms = ev0.elapsed_time(ev1) / max(1, steps)
+    for b in batches:
+        assert (b.status_host() == 0).all(), "hash jobs reported an error status"
     wall = max_over_ranks(wall, device)  # the job takes as long as its slowest rank
 
-    total_bytes = world * nbytes * args.steps
-    value = total_bytes / wall / GiB
-    kernel_name = "deep_kernel" if (mode == MODE_DEEP or (mode == MODE_AUTO and n <= 1536)) else "wide_kernel"
-    workload_key = f"{n}x{chunk}:{'sha1' if args.sha1_only else 'sha1+crc32'}"
-    achieved = nbytes / (kernel_ms * 1e-3) / 1e9
-    traffic = load_traffic(kernel_name, workload_key)
+    bytes_timed = sum(step_bytes[k % len(step_bytes)] for k in range(steps))
+    value = world * bytes_timed / wall / GiB
+    njobs = batches[0].n
+    deep = mode == MODE_DEEP or (mode == MODE_AUTO and njobs <= kAutoDeepMaxJobs)
+    kernel_name = "deep_kernel" if deep else "wide_kernel"
+    per_launch = bytes_timed / steps
+    workload_key = f"{config['workload']}:{'sha1' if args.sha1_only else 'sha1+crc32'}"
+    if args.workload == "chunks4m":
+        workload_key = f"{njobs}x{args.chunk_bytes}:{'sha1' if args.sha1_only else 'sha1+crc32'}"
+    achieved = per_launch / (kernel_ms * 1e-3) / 1e9
+    config.update({"kernel": kernel_name, "parallelism": f"per-GPU queues x{world}, no collectives"})
     out = {
         "metric": METRIC,
         "value": round(value, 3),
         "unit": "GiB/s",
         "n_gpus": world,
-        "steps": args.steps,
+        "steps": steps,
         "warmup": args.warmup,
-        "ms_per_step": round(wall * 1e3 / args.steps, 4),
+        "ms_per_step": round(wall * 1e3 / steps, 4),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u32",
         "data": "synthetic (device-generated splitmix64 bytes)",
-        "config": {
-            "workload": ("1024 x 4 MiB chunks, SHA-1 only (BASELINE configs[1])" if args.sha1_only else
-                         "1024 x 4 MiB chunks, fused single-pass SHA-1 + CRC32 (BASELINE configs[2])")
-            if (n, chunk) == (1024, 4 << 20) else f"{n} x {chunk} B chunks",
-            "chunks_per_gpu": n,
-            "chunk_bytes": chunk,
-            "kernel": kernel_name,
-            "parallelism": f"per-GPU queues x{world}, no collectives",
-        },
+        "config": config,
         "roofline": {
             "bound": "hbm",
             "achieved": round(achieved, 2),
             "peak": HBM_PEAK_GBPS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 5),
-            "traffic": traffic,
+            "traffic": load_traffic(kernel_name, workload_key),
             "kernel_ms": round(kernel_ms, 4),
-            "algorithmic_bytes_per_launch": nbytes,
+            "algorithmic_bytes_per_launch": int(per_launch),
         },
         "cpu_baseline": None,
     }
-    if args.host_inclusive == "on" or (args.host_inclusive == "auto" and world == 1):
-        out["host_inclusive"] = host_inclusive(ctx, data, n, chunk, not args.sha1_only, args.segment_bytes, batch)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        threads = args.cpu_threads or host_threads()
-        out["cpu_baseline"] = cpu_baseline(batch, data, min(n, args.cpu_max_chunks), chunk, threads, not args.sha1_only,
-                                           args.cpu_seconds)
+    if args.workload == "chunks4m":
+        n, chunk = args.chunks, args.chunk_bytes
+        if args.host_inclusive == "on" or (args.host_inclusive == "auto" and world == 1):
+            out["host_inclusive"] = host_inclusive(ctx, data, n, chunk, not args.sha1_only, args.segment_bytes,
+                                                   batches[0])
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            threads = args.cpu_threads or host_threads()
+            out["cpu_baseline"] = cpu_baseline(batches[0], data, min(n, args.cpu_max_chunks), chunk, threads,
+                                               not args.sha1_only, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:

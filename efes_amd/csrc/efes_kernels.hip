@@ -82,6 +82,16 @@ __device__ __forceinline__ uint32_t be_word_lds(const uint8_t* b, int k) {
   return (uint32_t)b[4 * k] << 24 | (uint32_t)b[4 * k + 1] << 16 | (uint32_t)b[4 * k + 2] << 8 | b[4 * k + 3];
 }
 
+// Message bytes are always device global memory: address-space-1 pointers make the compiler
+// emit global_load (counted by vmcnt only) instead of flat_load, which also counts in
+// lgkmcnt and would make every LDS wait of the chain wait for the in-flight prefetch too.
+#define EFES_GLOBAL __attribute__((address_space(1)))
+template <class T>
+__device__ __forceinline__ const EFES_GLOBAL T* gptr(const T* p) {
+  return (const EFES_GLOBAL T*)p;
+}
+__device__ __forceinline__ uint32_t ldg_u8(const uint8_t* p) { return *gptr(p); }
+
 // Load 64 bytes at an arbitrary device address as 16 little-endian words.
 // kAligned16: the address is 16-byte aligned (4 x global_load_dwordx4).
 // Otherwise: 16 (or 17) naturally aligned dword loads funnel-shifted by v_alignbyte.  The
@@ -90,15 +100,16 @@ __device__ __forceinline__ uint32_t be_word_lds(const uint8_t* b, int k) {
 template <bool kAligned16>
 __device__ __forceinline__ void load_block_le(const uint8_t* src, uint32_t (&le)[16]) {
   if constexpr (kAligned16) {
-    const uint4* s = reinterpret_cast<const uint4*>(src);
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    const EFES_GLOBAL v4u* s = gptr(reinterpret_cast<const v4u*>(src));
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const uint4 v = s[q];
+      const v4u v = s[q];
       le[4 * q] = v.x; le[4 * q + 1] = v.y; le[4 * q + 2] = v.z; le[4 * q + 3] = v.w;
     }
   } else {
     const uintptr_t a = reinterpret_cast<uintptr_t>(src);
-    const uint32_t* s = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+    const EFES_GLOBAL uint32_t* s = gptr(reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3));
     const uint32_t sh = (uint32_t)(a & 3);
     uint32_t d[17];
 #pragma unroll
@@ -229,7 +240,7 @@ __device__ void deep_job(DeepLDS& L, int wave, int lane, const DeepJob& J) {
   if (do_sha && nx > 0) {
     const uint32_t room = (uint32_t)(64 - nx);
     const uint32_t nh = plen < room ? (uint32_t)plen : room;
-    if ((uint32_t)lane < nh) xs[nx + lane] = *EFES_RANGE(p + lane, 1, p, plen, "deep-head");
+    if ((uint32_t)lane < nh) xs[nx + lane] = ldg_u8(EFES_RANGE(p + lane, 1, p, plen, "deep-head"));
     wave_lds_sync();
     if ((uint32_t)nx + nh == 64) {
       uint32_t w[16];
@@ -243,7 +254,7 @@ __device__ void deep_job(DeepLDS& L, int wave, int lane, const DeepJob& J) {
     pos = nh;
   }
   if (do_crc)
-    for (uint64_t i = 0; i < pos; ++i) crc_raw = crc_byte(L.tab.slice8[0], crc_raw, *EFES_RANGE(p + i, 1, p, plen, "deep-crchead"));
+    for (uint64_t i = 0; i < pos; ++i) crc_raw = crc_byte(L.tab.slice8[0], crc_raw, ldg_u8(EFES_RANGE(p + i, 1, p, plen, "deep-crchead")));
 
   // ---- bulk whole blocks (sha1.go:70-74)
   const uint8_t* q = p + pos;
@@ -259,9 +270,9 @@ __device__ void deep_job(DeepLDS& L, int wave, int lane, const DeepJob& J) {
   const uint64_t tpos = pos + (nbulk << 6);
   const uint32_t r = (uint32_t)(plen - tpos);
   if (do_crc)
-    for (uint32_t i = 0; i < r; ++i) crc_raw = crc_byte(L.tab.slice8[0], crc_raw, *EFES_RANGE(p + tpos + i, 1, p, plen, "deep-crctail"));
+    for (uint32_t i = 0; i < r; ++i) crc_raw = crc_byte(L.tab.slice8[0], crc_raw, ldg_u8(EFES_RANGE(p + tpos + i, 1, p, plen, "deep-crctail")));
   if (do_sha && r > 0) {
-    if ((uint32_t)lane < r) xs[lane] = *EFES_RANGE(p + tpos + lane, 1, p, plen, "deep-tail");
+    if ((uint32_t)lane < r) xs[lane] = ldg_u8(EFES_RANGE(p + tpos + lane, 1, p, plen, "deep-tail"));
     nx_new = r;
   }
   wave_lds_sync();
@@ -381,6 +392,35 @@ __device__ __forceinline__ uint32_t fin_byte(const uint8_t* xl, uint32_t i, uint
   return 0u;
 }
 
+__device__ __forceinline__ void wide_block(const uint32_t (&le)[16], bool do_sha, bool do_crc,
+                                           const uint32_t (&t)[8][256], uint32_t (&h)[5], uint32_t& crc_raw) {
+  if (do_crc) crc_raw = crc_words_raw(t, crc_raw, le);
+  if (do_sha) {
+    uint32_t w[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) w[k] = bswap(le[k]);
+    compress_inline(h, w);
+  }
+}
+
+// Whole blocks of one lane's message, software-pipelined: block b+1 is in flight while block
+// b is compressed (a lone uncoalesced 64-B load per lane would otherwise expose the full
+// memory latency every block).  Lanes run their own trip counts; with jobs sorted by length
+// the lanes of a wave finish together.
+template <bool kAligned16>
+__device__ __forceinline__ void wide_bulk(const uint8_t* q, uint64_t nbulk, bool do_sha, bool do_crc,
+                                          const uint32_t (&t)[8][256], uint32_t (&h)[5], uint32_t& crc_raw) {
+  uint32_t A[16], B[16];
+  if (nbulk) load_block_le<kAligned16>(q, A);
+  for (uint64_t b = 0; b < nbulk; b += 2) {
+    if (b + 1 < nbulk) load_block_le<kAligned16>(q + 64 * (b + 1), B);
+    wide_block(A, do_sha, do_crc, t, h, crc_raw);
+    if (b + 1 >= nbulk) break;
+    if (b + 2 < nbulk) load_block_le<kAligned16>(q + 64 * (b + 2), A);
+    wide_block(B, do_sha, do_crc, t, h, crc_raw);
+  }
+}
+
 __global__ __launch_bounds__(64 * kWideWaves, 2) void wide_kernel(const efes_job* __restrict__ jobs, uint32_t njobs,
                                                                   const Tables* __restrict__ tabs) {
   __shared__ __attribute__((aligned(16))) WideLDS L;
@@ -431,7 +471,7 @@ __global__ __launch_bounds__(64 * kWideWaves, 2) void wide_kernel(const efes_job
   if (go && do_sha && nx > 0) {
     const uint32_t room = (uint32_t)(64 - nx);
     const uint32_t nh = plen < room ? (uint32_t)plen : room;
-    for (uint32_t i = 0; i < nh; ++i) xl[nx + i] = p[i];
+    for (uint32_t i = 0; i < nh; ++i) xl[nx + i] = ldg_u8(p + i);
     if ((uint32_t)nx + nh == 64) {
       uint32_t w[16];
 #pragma unroll
@@ -444,32 +484,22 @@ __global__ __launch_bounds__(64 * kWideWaves, 2) void wide_kernel(const efes_job
     pos = nh;
   }
   if (go && do_crc)
-    for (uint64_t i = 0; i < pos; ++i) crc_raw = crc_byte(L.slice8[0], crc_raw, p[i]);
+    for (uint64_t i = 0; i < pos; ++i) crc_raw = crc_byte(L.slice8[0], crc_raw, ldg_u8(p + i));
 
   // ---- bulk: lanes iterate their own block counts (masked when done)
   const uint8_t* q = p + pos;
   const uint64_t nbulk = go ? (plen - pos) >> 6 : 0;
   const bool all16 = __all(!go || (reinterpret_cast<uintptr_t>(q) & 15) == 0);
-  for (uint64_t b = 0; b < nbulk; ++b) {
-    uint32_t le[16];
-    if (all16) load_block_le<true>(q + 64 * b, le);
-    else load_block_le<false>(q + 64 * b, le);
-    if (do_crc) crc_raw = crc_words_raw(L.slice8, crc_raw, le);
-    if (do_sha) {
-      uint32_t w[16];
-#pragma unroll
-      for (int k = 0; k < 16; ++k) w[k] = bswap(le[k]);
-      compress_inline(h, w);
-    }
-  }
+  if (all16) wide_bulk<true>(q, nbulk, do_sha, do_crc, L.slice8, h, crc_raw);
+  else wide_bulk<false>(q, nbulk, do_sha, do_crc, L.slice8, h, crc_raw);
 
   // ---- tail
   const uint64_t tpos = pos + (nbulk << 6);
   const uint32_t r = go ? (uint32_t)(plen - tpos) : 0u;
   if (do_crc)
-    for (uint32_t i = 0; i < r; ++i) crc_raw = crc_byte(L.slice8[0], crc_raw, p[tpos + i]);
+    for (uint32_t i = 0; i < r; ++i) crc_raw = crc_byte(L.slice8[0], crc_raw, ldg_u8(p + tpos + i));
   if (do_sha && r > 0) {
-    for (uint32_t i = 0; i < r; ++i) xl[i] = p[tpos + i];
+    for (uint32_t i = 0; i < r; ++i) xl[i] = ldg_u8(p + tpos + i);
     nx_new = r;
   }
   len += go ? plen : 0;

@@ -175,3 +175,20 @@ def test_hash_many_threads(oracle):
         assert bytes(sha[i]).hex() == hashlib.sha1(m).hexdigest()
         assert crc[i] == zlib.crc32(m)
     assert secs >= 0
+
+
+def test_chunksize_mirrors_go():
+    """chunksize.go Set/String semantics (benchmark size classes come from these)."""
+    from efes_amd import chunksize as c
+    assert c.parse("1M") == 1 << 20 and c.parse("50M") == 50 << 20 and c.parse("64K") == 65536
+    assert c.parse("0") == 0 and c.parse("123") == 123 and c.parse("2G") == 2 << 30 and c.parse("-1K") == -1024
+    assert c.parse("9223372036854775807K") == -1024  # int64 wrap-around of i *= K
+    for bad in ("1.5M", "M", "1 M", "x", "1KB", "99999999999999999999"):
+        with pytest.raises(ValueError):
+            c.parse(bad)
+    with pytest.raises(IndexError):
+        c.parse("")
+    assert [c.format(v) for v in (0, 1536, 2048, 1 << 20, 3 << 30, -2048, 1)] == \
+        ["0", "1536", "2K", "1M", "3G", "-2K", "1"]
+    assert [c.format(v) for v in c.MIXED_CLASSES] == ["64K", "128K", "256K", "512K", "1M", "2M", "4M", "8M",
+                                                       "16M", "32M", "64M"]

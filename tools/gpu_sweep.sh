@@ -1,5 +1,8 @@
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
-for args in "--sha1-only" "--chunks 65536 --chunk-bytes 65536 --mode wide" "--chunks 262144 --chunk-bytes 16384 --mode wide" "--chunks 16384 --chunk-bytes 262144 --mode wide" "--chunks 16384 --chunk-bytes 262144 --mode deep"; do
-  timeout -k 10 300 python bench.py --no-cpu-baseline --steps 5 --warmup 1 $args > gpurun_out/b.json 2> gpurun_out/b.err || { echo "FAIL $args"; tail -5 gpurun_out/b.err; exit 1; }
-  python -c "import json;d=json.load(open('gpurun_out/b.json'));print('$args', d['value'], 'GiB/s', d['roofline']['kernel_ms'],'ms', d['config']['kernel'])"
-done
+run() {  # run one bench configuration, print a summary line; stop the sweep on any failure
+  timeout -k 10 ${T:-300} python bench.py --no-cpu-baseline --host-inclusive off "$@" > gpurun_out/b.json 2> gpurun_out/b.err || { echo "FAIL $*"; tail -5 gpurun_out/b.err; exit 1; }
+  python -c "import json,sys;d=json.load(open('gpurun_out/b.json'));print(sys.argv[1:], d['value'], 'GiB/s', d['roofline']['kernel_ms'],'ms/launch', d['steps'], 'steps', d['config']['kernel'], d['config'].get('bytes_per_gpu',''))" "$@"
+  cp gpurun_out/b.json "gpurun_out/sweep_$(echo "$*" | tr ' -' '__').json"
+}
+for spec in "$@"; do eval run $spec; done
+echo SWEEP_DONE

@@ -58,6 +58,46 @@ __global__ __launch_bounds__(64) void ks(const uint32_t* __restrict__ g, uint32_
   if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
 }
 
+// ---- scalar-fed chain: WK streamed into SGPRs by s_load (glc: straight from L2), one quarter
+// (20 words) ahead, double-buffered.  SMEM returns out of order, so each wait is lgkmcnt(0);
+// the wait names the buffer it guards ("+s") so no use of it can be scheduled above it.
+typedef uint32_t v16u __attribute__((ext_vector_type(16)));
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+struct QBuf { v16u a; v4u b; };
+__device__ __forceinline__ void sload_q(QBuf& q, const uint32_t* p) {
+  asm volatile("s_load_dwordx16 %0, %2, 0x0 glc\n\ts_load_dwordx4 %1, %2, 0x40 glc" : "=s"(q.a), "=s"(q.b) : "s"(p) : "memory");
+}
+__device__ __forceinline__ void swait_q(QBuf& q) { asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(q.a), "+s"(q.b) :: "memory"); }
+template <int Q, int I> struct SQ20 {
+  __device__ __forceinline__ static void run(uint32_t (&s)[5], const QBuf& w) {
+    round_wk<20 * Q + I>(s, I < 16 ? w.a[I & 15] : w.b[(I - 16) & 3]);
+    SQ20<Q, I + 1>::run(s, w);
+  }
+};
+template <int Q> struct SQ20<Q, 20> { __device__ __forceinline__ static void run(uint32_t (&)[5], const QBuf&) {} };
+
+__global__ __launch_bounds__(64) void kq(const uint32_t* __restrict__ g, uint32_t* out, uint64_t* cyc, int nblocks) {
+  uint32_t h[5] = {0x67452301u + blockIdx.x, 0xEFCDAB89u, 0x98BADCFEu, 0x10325476u, 0xC3D2E1F0u};
+  const uint32_t* base = g;
+  uint64_t t0 = __builtin_amdgcn_s_memtime();
+  QBuf A, B;
+  sload_q(A, base);
+  for (int b = 0; b < nblocks; ++b) {
+    const uint32_t* w = base + (b & 63) * 80;
+    const uint32_t* wn = base + ((b + 1) & 63) * 80;
+    uint32_t s[5] = {h[0], h[1], h[2], h[3], h[4]};
+    swait_q(A); sload_q(B, w + 20); SQ20<0, 0>::run(s, A);
+    swait_q(B); sload_q(A, w + 40); SQ20<1, 0>::run(s, B);
+    swait_q(A); sload_q(B, w + 60); SQ20<2, 0>::run(s, A);
+    swait_q(B); sload_q(A, wn);     SQ20<3, 0>::run(s, B);
+    h[0] += s[0]; h[1] += s[1]; h[2] += s[2]; h[3] += s[3]; h[4] += s[4];
+  }
+  swait_q(A);
+  uint64_t t1 = __builtin_amdgcn_s_memtime();
+  out[blockIdx.x * 64 + threadIdx.x] = h[0] ^ h[1] ^ h[2] ^ h[3] ^ h[4];
+  if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
+}
+
 template <int MODE>
 __global__ __launch_bounds__(64) void k(uint32_t* out, uint64_t* cyc, int nblocks) {
   __shared__ __attribute__((aligned(16))) uint4 ring[64][20];
@@ -148,6 +188,6 @@ int main() {
     return 0;
   };
   for (int g : {1, 1024}) { run("regs", k<0>, g); run("lds", k<1>, g); run("pipe", k<2>, g); run("lds16", k<3>, g); run("lds1", k<4>, g); run("pipe1", k<5>, g);
-                            runs("smem4", ks<4>, g); runs("smem64", ks<64>, g); }
+                            runs("smem4", ks<4>, g); runs("smem64", ks<64>, g); runs("squarter", kq, g); }
   return 0;
 }

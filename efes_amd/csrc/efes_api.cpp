@@ -357,6 +357,28 @@ int efes_crc32_tables(uint32_t* out, size_t nwords) {
   return (int)need;
 }
 
+uint32_t efes_crc32_combine(uint32_t crc1, uint32_t crc2, uint64_t len2) {
+  // Raw register update over B is affine: R(x, B) = Z^|B| x ^ R(0, B), Z = one zero byte
+  // (crc32.go:125).  With crc(X) = ~R(~0, X) (crc32.go:123,127):
+  //   crc(A||B) ^ crc(B) = Z^|B|(~crc(A)) ^ Z^|B|(~0) = Z^|B|(crc(A)).
+  if (len2 == 0) return crc1;
+  Gf2 z;
+  for (int i = 0; i < 32; ++i) {
+    const uint32_t s = 1u << i;
+    uint32_t c = s;
+    c = (c & 1) ? (c >> 1) ^ 0xedb88320u : c >> 1;  // one zero bit, eight times = one zero byte
+    for (int k = 1; k < 8; ++k) c = (c & 1) ? (c >> 1) ^ 0xedb88320u : c >> 1;
+    z.col[i] = c;
+  }
+  uint32_t v = crc1;
+  Gf2 p = z;  // Z^(2^k)
+  for (uint64_t n = len2; n; n >>= 1) {
+    if (n & 1) v = p.apply(v);
+    p = compose(p, p);
+  }
+  return v ^ crc2;
+}
+
 // ---- text codecs --------------------------------------------------------------------------
 void efes_sha1_state_marshal_text(const efes_sha1_state* s, char out[200]) {  // sha1_efes.go:25-38
   uint8_t b[100];

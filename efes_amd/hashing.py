@@ -23,7 +23,7 @@ import threading
 
 from ._lib import MODE_AUTO, EfesError, Sha1State, check, lib
 
-__all__ = ["Context", "default_context", "Sha1Digest", "CRC32Digest", "Sha1File", "Digest", "FileInfo",
+__all__ = ["Context", "default_context", "crc32_combine", "Sha1Digest", "CRC32Digest", "Sha1File", "Digest", "FileInfo",
            "new_sha1", "new_crc32_ieee", "EfesError"]
 
 
@@ -77,6 +77,11 @@ def default_context(device: int = 0) -> Context:
         if device not in _contexts:
             _contexts[device] = Context(device)
         return _contexts[device]
+
+
+def crc32_combine(crc1: int, crc2: int, len2: int) -> int:
+    """CRC-32 of A||B from crc(A), crc(B), |B| (efes_crc32_combine; crc32.go is GF(2)-linear)."""
+    return int(lib().efes_crc32_combine(crc1 & 0xFFFFFFFF, crc2 & 0xFFFFFFFF, len2))
 
 
 def _as_bytes(p) -> bytes:

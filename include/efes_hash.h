@@ -176,6 +176,11 @@ int efes_crc32_unmarshal_text(efes_crc32* d, const char* text, size_t n);/* crc3
  * over 64<<k zero bytes, byte-sliced); returns the word count written or EFES_ERR_ARG. */
 int efes_crc32_tables(uint32_t* out, size_t nwords);
 
+/* CRC-32 of A||B from crc(A), crc(B) and |B| (crc32.go is GF(2)-linear: the zlib
+ * crc32_combine identity), so chunks of one object can be CRC'd out of order or on different
+ * devices and merged on the host; len2 may be any size (O(log len2) 32x32 GF(2) products). */
+uint32_t efes_crc32_combine(uint32_t crc1, uint32_t crc2, uint64_t len2);
+
 /* Pure text codecs on plain states (no device work). */
 void efes_sha1_state_marshal_text(const efes_sha1_state* s, char out[200]);
 int efes_sha1_state_unmarshal_text(efes_sha1_state* s, const char* text, size_t n);

@@ -118,3 +118,20 @@ def test_no_gpu_is_an_error_not_a_fallback(efes_lib):
     rc = efes_lib.lib().efes_ctx_create(0, ctypes.byref(h))
     assert rc == efes_lib.EFES_ERR_NO_DEVICE and not h.value
     assert efes_lib.lib().efes_strerror(rc) == b"no usable gfx950 device"
+
+
+def test_crc32_combine_matches_concatenation(efes_lib):
+    """efes_crc32_combine == zlib crc32 of the concatenation (crc32.go linearity)."""
+    import random
+    import zlib
+    L = efes_lib.lib()
+    rng = random.Random(4)
+    for la, lb in [(0, 0), (0, 5), (5, 0), (1, 1), (63, 65), (4096, 1 << 20), (rng.randint(0, 99999), 12345)]:
+        a, b = rng.randbytes(la), rng.randbytes(lb)
+        assert L.efes_crc32_combine(zlib.crc32(a), zlib.crc32(b), lb) == zlib.crc32(a + b)
+    # associativity over huge lengths (no data needed): ((a+b)+c) == (a+(b+c))
+    ca, cb, cc = 0x12345678, 0x9ABCDEF0, 0x0F1E2D3C
+    lb, lc = (1 << 40) + 3, (10 << 40) + 77
+    left = L.efes_crc32_combine(L.efes_crc32_combine(ca, cb, lb), cc, lc)
+    right = L.efes_crc32_combine(ca, L.efes_crc32_combine(cb, cc, lc), lb + lc)
+    assert left == right

@@ -83,6 +83,14 @@ SIGNATURES = {
     "efes_hash_host": (_I, [_VP, _VP, _U32, _U64, _P(HostStats)]),
     "efes_host_alloc": (_I, [_VP, _S, _P(_VP)]),
     "efes_host_free": (_I, [_VP, _VP]),
+    "efes_queue_create": (_I, [_VP, _U64, _U32, _U32, _P(_VP)]),
+    "efes_queue_destroy": (None, [_VP]),
+    "efes_upload_open": (_I, [_VP, _P(Sha1State), _P(Crc32State), _P(_VP)]),
+    "efes_upload_write": (_I, [_VP, _VP, _S]),
+    "efes_upload_flush": (_I, [_VP]),
+    "efes_upload_state": (_I, [_VP, _P(Sha1State), _P(Crc32State)]),
+    "efes_upload_sum": (_I, [_VP, _VP]),
+    "efes_upload_close": (None, [_VP]),
     "efes_sha1_new": (_I, [_VP, _P(_VP)]),
     "efes_sha1_new_zero": (_I, [_VP, _P(_VP)]),
     "efes_sha1_free": (None, [_VP]),

@@ -76,29 +76,6 @@ void put_be64(uint8_t* b, uint64_t v) { for (int i = 0; i < 8; ++i) b[i] = (uint
 uint32_t get_be32(const uint8_t* b) { return (uint32_t)b[0] << 24 | (uint32_t)b[1] << 16 | (uint32_t)b[2] << 8 | b[3]; }
 uint64_t get_be64(const uint8_t* b) { uint64_t v = 0; for (int i = 0; i < 8; ++i) v = v << 8 | b[i]; return v; }
 
-// Go's sha1digest.Write bookkeeping of x/nx/len (sha1.go:58-79) without the compressions.
-int replay_write(efes_sha1_state* s, const uint8_t* p, size_t n) {
-  if (s->nx > 64) return EFES_ERR_STATE;  // copy(d.x[d.nx:], p) panics
-  s->len += (uint64_t)n;
-  if (s->nx > 0) {
-    const size_t room = (size_t)(64 - s->nx);
-    const size_t c = n < room ? n : room;
-    memcpy(s->x + s->nx, p, c);
-    s->nx += (int64_t)c;
-    if (s->nx == 64) s->nx = 0;
-    p += c;
-    n -= c;
-  }
-  const size_t m = n & ~(size_t)63;
-  p += m;
-  n -= m;
-  if (n > 0) {
-    memcpy(s->x, p, n);
-    s->nx = (int64_t)n;
-  }
-  return EFES_OK;
-}
-
 // Device scratch of one streaming object: [job 56 | pad | sha1 state 104 | crc 4 | sum 24 | status 4].
 struct DevScratch {
   uint8_t* base = nullptr;
@@ -179,6 +156,32 @@ struct Staged {
 };
 
 }  // namespace
+
+namespace efes {
+// Go's sha1digest.Write bookkeeping of x/nx/len (sha1.go:58-79) without the compressions.
+int replay_write(efes_sha1_state* s, const uint8_t* p, size_t n) {
+  if (s->nx > 64) return EFES_ERR_STATE;  // copy(d.x[d.nx:], p) panics
+  s->len += (uint64_t)n;
+  if (s->nx > 0) {
+    const size_t room = (size_t)(64 - s->nx);
+    const size_t c = n < room ? n : room;
+    memcpy(s->x + s->nx, p, c);
+    s->nx += (int64_t)c;
+    if (s->nx == 64) s->nx = 0;
+    p += c;
+    n -= c;
+  }
+  const size_t m = n & ~(size_t)63;
+  p += m;
+  n -= m;
+  if (n > 0) {
+    memcpy(s->x, p, n);
+    s->nx = (int64_t)n;
+  }
+  return EFES_OK;
+}
+}  // namespace efes
+using efes::replay_write;
 
 struct efes_sha1 {
   Staged stg;

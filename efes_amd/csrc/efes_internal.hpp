@@ -23,6 +23,10 @@ struct Tables {
 
 void build_tables(Tables* t);  // host
 
+// Go's sha1digest.Write bookkeeping of x/nx/len (sha1.go:58-79) without the compressions:
+// the host replays it so exported states carry Go's exact tail bytes (efes_api.cpp).
+int replay_write(efes_sha1_state* s, const uint8_t* p, size_t n);
+
 // Launchers (host side, defined in efes_kernels.hip).
 hipError_t launch_deep(const efes_job* jobs, uint32_t njobs, const Tables* tabs, hipStream_t s);
 hipError_t launch_wide(const efes_job* jobs, uint32_t njobs, const Tables* tabs, hipStream_t s);

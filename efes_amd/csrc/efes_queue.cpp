@@ -1,0 +1,410 @@
+// efes_queue.cpp -- batching dispatcher for concurrent uploads.
+//
+// The reference hashes each upload in its own request goroutine (server.go:130): every
+// io.Copy buffer goes through MultiWriter(file, CRC32, Sha1) (filereceiver.go:208-209) and
+// the digest is read at the end of the PATCH (Sum, filereceiver.go:99-100) or saved to the
+// .info file (MarshalText, filereceiver.go:226).  On the GPU one launch must carry many
+// uploads, so an efes_upload is the device-resident (SHA-1, CRC-32) pair of one upload, its
+// Write copies into pinned staging and returns, and a dispatcher thread per queue turns the
+// staged chunks of all uploads into one kernel launch (at most one chunk per upload per
+// launch, so each upload's chain stays in order on the queue's stream) while callers keep
+// staging.  Sync points (flush / state / sum) wait for that upload's bytes only.
+//
+// Tail-buffer bytes x/nx/len are replayed on the host per Write (efes::replay_write), so an
+// exported state is byte-identical to what Go's MarshalText would write after the same
+// Write calls, stale bytes included; h and crc come from the device.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <condition_variable>
+#include <deque>
+#include <mutex>
+#include <new>
+#include <thread>
+#include <vector>
+
+#include "efes_internal.hpp"
+
+using efes::DeviceGuard;
+
+namespace {
+// Device slot of one upload: sha1 state 104 | crc 4 | pad | sum 24 | status 4 | pad | job 56.
+constexpr size_t kDevStateBytes = 256;
+constexpr size_t kOffCrc = 104, kOffSum = 112, kOffStatus = 136, kOffJob = 144;
+}  // namespace
+
+struct efes_upload {
+  efes_queue* q = nullptr;
+  uint32_t dslot = 0;            // device state slot
+  int32_t cur = -1;              // staging chunk being filled (-1: none)
+  uint64_t fill = 0;             // bytes in `cur`
+  uint64_t inflight = 0;         // chunks queued or running
+  bool in_batch = false;         // has a chunk in the batch being assembled
+  int latched = EFES_OK;         // first device / state error
+  efes_sha1_state shadow{};      // Go's x/nx/len after every Write (h from the device)
+  std::condition_variable done;  // inflight reached 0
+};
+
+struct Pending {
+  efes_upload* u;
+  uint32_t slot;
+  uint64_t len;
+};
+
+struct Batch {
+  hipEvent_t ev = nullptr;
+  std::vector<Pending> items;
+  int jobs_half = 0;
+};
+
+struct efes_queue {
+  efes_ctx* ctx = nullptr;
+  uint64_t chunk = 0;
+  uint32_t nchunks = 0, max_uploads = 0;
+  uint8_t* h_slab = nullptr;       // pinned staging, nchunks x chunk
+  uint8_t* d_slab = nullptr;       // device mirror
+  uint8_t* d_states = nullptr;     // max_uploads x kDevStateBytes
+  efes_job* h_jobs = nullptr;      // pinned, 2 halves x nchunks
+  efes_job* d_jobs = nullptr;
+  hipStream_t stream = nullptr, ctl = nullptr;
+  std::mutex mu;
+  std::condition_variable work, freed;
+  std::vector<uint32_t> free_chunks, free_states;
+  std::deque<Pending> pending;
+  std::deque<Batch> running;
+  int next_half = 0;
+  bool stop = false;
+  int fault = EFES_OK;
+  std::thread th;
+
+  void run();
+  void retire(Batch& b, std::unique_lock<std::mutex>& lk);
+};
+
+// Waits for the batch (without holding mu, so callers keep staging) and releases its chunks.
+void efes_queue::retire(Batch& b, std::unique_lock<std::mutex>& lk) {  // mu held on entry and exit
+  lk.unlock();
+  const bool ok = hipEventSynchronize(b.ev) == hipSuccess;
+  (void)hipEventDestroy(b.ev);
+  lk.lock();
+  if (!ok && fault == EFES_OK) fault = EFES_ERR_DEVICE_FAULT;
+  for (const Pending& p : b.items) {
+    free_chunks.push_back(p.slot);
+    if (!ok) p.u->latched = EFES_ERR_DEVICE_FAULT;
+    if (--p.u->inflight == 0) p.u->done.notify_all();
+  }
+  freed.notify_all();
+}
+
+void efes_queue::run() {
+  DeviceGuard g(ctx->device);
+  std::unique_lock<std::mutex> lk(mu);
+  for (;;) {
+    work.wait(lk, [&] { return stop || !pending.empty() || !running.empty(); });
+    if (pending.empty()) {
+      if (running.empty()) {
+        if (stop) return;
+        continue;
+      }
+      Batch b = std::move(running.front());  // nothing new to launch: retire the oldest
+      running.pop_front();
+      retire(b, lk);
+      continue;
+    }
+    if (running.size() >= 2) {  // two launches in flight: their job-array halves are busy
+      Batch b = std::move(running.front());
+      running.pop_front();
+      retire(b, lk);
+      continue;
+    }
+    // Assemble: FIFO order, at most one chunk per upload (a job must not race its own state).
+    Batch b;
+    b.jobs_half = next_half;
+    next_half ^= 1;
+    std::deque<Pending> later;
+    while (!pending.empty()) {
+      Pending p = pending.front();
+      pending.pop_front();
+      if (p.u->in_batch) {
+        later.push_back(p);
+        continue;
+      }
+      p.u->in_batch = true;
+      b.items.push_back(p);
+    }
+    pending.swap(later);
+    for (const Pending& p : b.items) p.u->in_batch = false;
+    efes_job* hj = h_jobs + (size_t)b.jobs_half * nchunks;
+    efes_job* dj = d_jobs + (size_t)b.jobs_half * nchunks;
+    for (size_t i = 0; i < b.items.size(); ++i) {
+      const Pending& p = b.items[i];
+      uint8_t* st = d_states + (size_t)p.u->dslot * kDevStateBytes;
+      efes_job& j = hj[i];
+      j.data = d_slab + (size_t)p.slot * chunk;
+      j.length = p.len;
+      j.sha1 = reinterpret_cast<efes_sha1_state*>(st);
+      j.crc32 = reinterpret_cast<efes_crc32_state*>(st + kOffCrc);
+      j.sum = nullptr;
+      j.status = reinterpret_cast<int32_t*>(st + kOffStatus);
+      j.flags = 0;
+      j._reserved = 0;
+    }
+    lk.unlock();  // callers keep staging while this batch is copied and launched
+    hipError_t e = hipSuccess;
+    for (size_t i = 0; i < b.items.size() && e == hipSuccess; ++i) {
+      // coalesce runs of consecutive full slots into one copy
+      size_t k = i;
+      while (k + 1 < b.items.size() && b.items[k + 1].slot == b.items[k].slot + 1 && b.items[k].len == chunk) ++k;
+      const uint64_t bytes = (uint64_t)(k - i) * chunk + b.items[k].len;
+      e = hipMemcpyAsync(d_slab + (size_t)b.items[i].slot * chunk, h_slab + (size_t)b.items[i].slot * chunk, bytes,
+                         hipMemcpyHostToDevice, stream);
+      i = k;
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(dj, hj, sizeof(efes_job) * b.items.size(), hipMemcpyHostToDevice, stream);
+    int rc = e == hipSuccess ? efes_hash_submit(ctx, dj, (uint32_t)b.items.size(), stream) : EFES_ERR_HIP;
+    if (rc == EFES_OK && hipEventCreateWithFlags(&b.ev, hipEventDisableTiming) != hipSuccess) rc = EFES_ERR_HIP;
+    if (rc == EFES_OK && hipEventRecord(b.ev, stream) != hipSuccess) rc = EFES_ERR_HIP;
+    lk.lock();
+    if (rc != EFES_OK) {
+      if (b.ev) (void)hipEventDestroy(b.ev);
+      if (fault == EFES_OK) fault = rc;
+      for (const Pending& p : b.items) {
+        free_chunks.push_back(p.slot);
+        p.u->latched = rc;
+        if (--p.u->inflight == 0) p.u->done.notify_all();
+      }
+      freed.notify_all();
+      continue;
+    }
+    running.push_back(std::move(b));
+  }
+}
+
+namespace {
+
+int enqueue_current(efes_upload* u, std::unique_lock<std::mutex>&) {  // q->mu held
+  efes_queue* q = u->q;
+  if (u->cur < 0 || u->fill == 0) return EFES_OK;
+  q->pending.push_back(Pending{u, (uint32_t)u->cur, u->fill});
+  ++u->inflight;
+  u->cur = -1;
+  u->fill = 0;
+  q->work.notify_one();
+  return EFES_OK;
+}
+
+int wait_idle(efes_upload* u) {
+  efes_queue* q = u->q;
+  std::unique_lock<std::mutex> lk(q->mu);
+  enqueue_current(u, lk);
+  u->done.wait(lk, [&] { return u->inflight == 0; });
+  return u->latched;
+}
+
+}  // namespace
+
+extern "C" {
+
+int efes_queue_create(efes_ctx* ctx, uint64_t chunk_bytes, uint32_t max_chunks, uint32_t max_uploads,
+                      efes_queue** out) {
+  // Every open upload may hold one partly filled chunk; with max_uploads < max_chunks at least
+  // one chunk is always free or queued, so a writer waiting for a chunk always makes progress.
+  if (!ctx || !out || max_chunks < 2 || max_uploads == 0 || max_uploads >= max_chunks) return EFES_ERR_ARG;
+  *out = nullptr;
+  efes_queue* q = new (std::nothrow) efes_queue;
+  if (!q) return EFES_ERR_NOMEM;
+  q->ctx = ctx;
+  q->chunk = chunk_bytes ? (chunk_bytes + 63) & ~uint64_t(63) : (uint64_t)1 << 20;
+  q->nchunks = max_chunks;
+  q->max_uploads = max_uploads;
+  DeviceGuard g(ctx->device);
+  hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&q->h_slab), q->chunk * max_chunks, hipHostMallocDefault);
+  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&q->d_slab), q->chunk * max_chunks);
+  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&q->d_states), kDevStateBytes * max_uploads);
+  if (e == hipSuccess)
+    e = hipHostMalloc(reinterpret_cast<void**>(&q->h_jobs), 2 * sizeof(efes_job) * max_chunks, hipHostMallocDefault);
+  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&q->d_jobs), 2 * sizeof(efes_job) * max_chunks);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&q->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&q->ctl, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    efes_queue_destroy(q);
+    return EFES_ERR_HIP;
+  }
+  for (uint32_t i = max_chunks; i-- > 0;) q->free_chunks.push_back(i);
+  for (uint32_t i = max_uploads; i-- > 0;) q->free_states.push_back(i);
+  try {
+    q->th = std::thread([q] { q->run(); });
+  } catch (...) {
+    efes_queue_destroy(q);
+    return EFES_ERR_NOMEM;
+  }
+  *out = q;
+  return EFES_OK;
+}
+
+void efes_queue_destroy(efes_queue* q) {
+  if (!q) return;
+  if (q->th.joinable()) {
+    {
+      std::lock_guard<std::mutex> lk(q->mu);
+      q->stop = true;
+    }
+    q->work.notify_all();
+    q->th.join();
+  }
+  DeviceGuard g(q->ctx->device);
+  if (q->stream) (void)hipStreamSynchronize(q->stream);
+  if (q->ctl) (void)hipStreamSynchronize(q->ctl);
+  if (q->h_slab) (void)hipHostFree(q->h_slab);
+  if (q->d_slab) (void)hipFree(q->d_slab);
+  if (q->d_states) (void)hipFree(q->d_states);
+  if (q->h_jobs) (void)hipHostFree(q->h_jobs);
+  if (q->d_jobs) (void)hipFree(q->d_jobs);
+  if (q->stream) (void)hipStreamDestroy(q->stream);
+  if (q->ctl) (void)hipStreamDestroy(q->ctl);
+  delete q;
+}
+
+int efes_upload_open(efes_queue* q, const efes_sha1_state* sha1, const efes_crc32_state* crc, efes_upload** out) {
+  if (!q || !out) return EFES_ERR_ARG;
+  *out = nullptr;
+  efes_upload* u = new (std::nothrow) efes_upload;
+  if (!u) return EFES_ERR_NOMEM;
+  u->q = q;
+  {
+    std::lock_guard<std::mutex> lk(q->mu);
+    if (q->free_states.empty()) {
+      delete u;
+      return EFES_ERR_NOMEM;
+    }
+    u->dslot = q->free_states.back();
+    q->free_states.pop_back();
+  }
+  if (sha1) {
+    u->shadow = *sha1;
+  } else {
+    memset(&u->shadow, 0, sizeof u->shadow);
+    efes_sha1_state_init(&u->shadow);  // NewSha1 (sha1.go:48-52)
+  }
+  uint8_t init[kDevStateBytes] = {};
+  memcpy(init, &u->shadow, sizeof u->shadow);
+  const uint32_t c = crc ? crc->crc : 0u;  // NewCRC32IEEE
+  memcpy(init + kOffCrc, &c, 4);
+  DeviceGuard g(q->ctx->device);
+  hipError_t e = hipMemcpyAsync(q->d_states + (size_t)u->dslot * kDevStateBytes, init, sizeof init,
+                                hipMemcpyHostToDevice, q->ctl);
+  if (e == hipSuccess) e = hipStreamSynchronize(q->ctl);
+  if (e != hipSuccess) {
+    efes_upload_close(u);
+    return EFES_ERR_HIP;
+  }
+  *out = u;
+  return EFES_OK;
+}
+
+int efes_upload_write(efes_upload* u, const void* p, size_t n) {
+  if (!u || (!p && n)) return EFES_ERR_ARG;
+  if (u->latched) return u->latched;
+  const int rc = efes::replay_write(&u->shadow, static_cast<const uint8_t*>(p), n);
+  if (rc) return u->latched = rc;  // the Go Write would panic (nx > 64)
+  efes_queue* q = u->q;
+  const uint8_t* src = static_cast<const uint8_t*>(p);
+  std::unique_lock<std::mutex> lk(q->mu);
+  while (n > 0) {
+    if (u->cur < 0) {
+      q->freed.wait(lk, [&] { return !q->free_chunks.empty() || q->fault; });  // back-pressure
+      if (q->fault) return u->latched = q->fault;
+      u->cur = (int32_t)q->free_chunks.back();
+      q->free_chunks.pop_back();
+      u->fill = 0;
+    }
+    const uint64_t take = std::min<uint64_t>(n, q->chunk - u->fill);
+    uint8_t* dst = q->h_slab + (size_t)u->cur * q->chunk + u->fill;
+    lk.unlock();  // the copy runs outside the lock; `cur` is owned by this upload
+    memcpy(dst, src, take);
+    lk.lock();
+    u->fill += take;
+    src += take;
+    n -= take;
+    if (u->fill == q->chunk) enqueue_current(u, lk);
+  }
+  return EFES_OK;
+}
+
+int efes_upload_flush(efes_upload* u) {
+  if (!u) return EFES_ERR_ARG;
+  return wait_idle(u);
+}
+
+int efes_upload_state(efes_upload* u, efes_sha1_state* sha1, efes_crc32_state* crc) {
+  if (!u) return EFES_ERR_ARG;
+  int rc = wait_idle(u);
+  if (rc) return rc;
+  efes_queue* q = u->q;
+  uint8_t st[kDevStateBytes];
+  DeviceGuard g(q->ctx->device);
+  hipError_t e = hipMemcpyAsync(st, q->d_states + (size_t)u->dslot * kDevStateBytes, sizeof st,
+                                hipMemcpyDeviceToHost, q->ctl);
+  if (e == hipSuccess) e = hipStreamSynchronize(q->ctl);
+  if (e != hipSuccess) return u->latched = EFES_ERR_DEVICE_FAULT;
+  int32_t status;
+  memcpy(&status, st + kOffStatus, 4);
+  if (status != EFES_OK) return u->latched = status;
+  if (sha1) {
+    *sha1 = u->shadow;  // x/nx/len: Go's, from the replay
+    memcpy(sha1->h, st, sizeof sha1->h);
+  }
+  if (crc) memcpy(&crc->crc, st + kOffCrc, 4);
+  return EFES_OK;
+}
+
+int efes_upload_sum(efes_upload* u, uint8_t out[24]) {
+  if (!u || !out) return EFES_ERR_ARG;
+  int rc = wait_idle(u);
+  if (rc) return rc;
+  efes_queue* q = u->q;
+  // A zero-length FINALIZE job on the control stream, kept in the upload's own device slot:
+  // Sum works on a copy (sha1.go:82-87), so the state stays as it is.
+  uint8_t* st = q->d_states + (size_t)u->dslot * kDevStateBytes;
+  efes_job job{};
+  job.data = nullptr;
+  job.length = 0;
+  job.sha1 = reinterpret_cast<efes_sha1_state*>(st);
+  job.crc32 = reinterpret_cast<efes_crc32_state*>(st + kOffCrc);
+  job.sum = st + kOffSum;
+  job.status = reinterpret_cast<int32_t*>(st + kOffStatus);
+  job.flags = EFES_JOB_FINALIZE;
+  uint8_t back[kOffStatus + 4 - kOffSum];
+  DeviceGuard g(q->ctx->device);
+  hipError_t e = hipMemcpyAsync(st + kOffJob, &job, sizeof job, hipMemcpyHostToDevice, q->ctl);
+  if (e == hipSuccess)
+    rc = efes_hash_submit_mode(q->ctx, reinterpret_cast<const efes_job*>(st + kOffJob), 1, q->ctl, EFES_MODE_DEEP);
+  if (e == hipSuccess && rc == EFES_OK) e = hipMemcpyAsync(back, st + kOffSum, sizeof back, hipMemcpyDeviceToHost, q->ctl);
+  if (e == hipSuccess) e = hipStreamSynchronize(q->ctl);
+  if (e != hipSuccess) return u->latched = EFES_ERR_DEVICE_FAULT;
+  if (rc != EFES_OK) return rc;
+  int32_t status;
+  memcpy(&status, back + (kOffStatus - kOffSum), 4);
+  if (status != EFES_OK) return status;  // EFES_ERR_STATE: sha1.go:108 would panic
+  memcpy(out, back, 24);
+  return EFES_OK;
+}
+
+void efes_upload_close(efes_upload* u) {
+  if (!u) return;
+  efes_queue* q = u->q;
+  {
+    std::unique_lock<std::mutex> lk(q->mu);
+    if (u->cur >= 0) {  // staged but never flushed: drop it
+      q->free_chunks.push_back((uint32_t)u->cur);
+      u->cur = -1;
+      q->freed.notify_all();
+    }
+    u->done.wait(lk, [&] { return u->inflight == 0; });  // kernels may still use the state slot
+    q->free_states.push_back(u->dslot);
+  }
+  delete u;
+}
+
+}  // extern "C"

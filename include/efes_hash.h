@@ -143,6 +143,31 @@ int efes_hash_host(efes_ctx* ctx, const efes_job* jobs_host, uint32_t njobs, uin
 int efes_host_alloc(efes_ctx* ctx, size_t bytes, void** out); /* pinned host memory (hipHostMalloc) */
 int efes_host_free(efes_ctx* ctx, void* p);
 
+/* ---- concurrent uploads: batching dispatcher ------------------------------------------
+ * An efes_upload is the MultiWriter(CRC32, Sha1) of ONE upload (filereceiver.go:208) with
+ * both states in HBM.  efes_upload_write copies into pinned staging (chunk_bytes pieces out
+ * of max_chunks; it blocks only when all are in use) and returns; the queue's dispatcher
+ * thread launches the staged chunks of ALL uploads together -- one job per upload per launch,
+ * so each upload's chain stays in order -- while callers keep staging.  Sync points wait for
+ * that upload's bytes only: flush; state (h/crc from the device, x/nx/len replayed on the host
+ * per Write, so MarshalText of it is byte-identical to Go's after the same Writes); sum
+ * (SHA-1 Sum || CRC Sum, non-destructive, sha1.go:82-87).  Uploads may be used from different
+ * threads concurrently; one upload must not be written from two threads at once (each Go
+ * digest belongs to one request goroutine, server.go:130).  max_uploads bounds open uploads
+ * and must be < max_chunks (each open upload may hold one partly filled chunk). */
+typedef struct efes_queue efes_queue;
+typedef struct efes_upload efes_upload;
+int efes_queue_create(efes_ctx* ctx, uint64_t chunk_bytes, uint32_t max_chunks, uint32_t max_uploads,
+                      efes_queue** out);
+void efes_queue_destroy(efes_queue* q); /* finishes launched work; close uploads first */
+/* sha1 / crc32: initial states (host), NULL = NewSha1() / NewCRC32IEEE() */
+int efes_upload_open(efes_queue* q, const efes_sha1_state* sha1, const efes_crc32_state* crc32, efes_upload** out);
+int efes_upload_write(efes_upload* u, const void* p, size_t n);
+int efes_upload_flush(efes_upload* u);
+int efes_upload_state(efes_upload* u, efes_sha1_state* sha1, efes_crc32_state* crc32);
+int efes_upload_sum(efes_upload* u, uint8_t out[24]);
+void efes_upload_close(efes_upload* u); /* drops bytes staged since the last sync point */
+
 /* ---- layer 2: streaming digests mirroring the Go surface ---------------------------- */
 typedef struct efes_sha1 efes_sha1;
 typedef struct efes_crc32 efes_crc32;

@@ -462,3 +462,86 @@ def test_host_ingest_pinned_strided_and_resume(env, oracle):
                 assert bytes(hb.sums[i][:20]) == e_sum
     finally:
         buf.free()
+
+
+# ---------------------------------------------------------------- concurrent uploads (efes_queue)
+
+def test_upload_queue_concurrent_threads(env, oracle):
+    """16 threads, 48 uploads, io.Copy-like Write sizes; sums and MarshalText equal the oracle's
+    after the SAME Write calls (stale tail bytes included)."""
+    import threading
+    from efes_amd.uploads import UploadQueue
+    rng = random.Random(21)
+    plans = []
+    for u in range(48):
+        total = rng.choice([0, 1, 63, 64, 65, 1000, 70000, 1 << 20, (3 << 20) + 7, rng.randint(0, 5 << 20)])
+        data = oracle.fill_synthetic(total, 1000 + u).tobytes()
+        cuts, pos = [], 0
+        while pos < total:
+            n = min(total - pos, rng.choice([1, 7, 64, 4096, 32 * 1024, 32 * 1024, 200000]))
+            cuts.append((pos, n))
+            pos += n
+        plans.append((data, cuts))
+    results = [None] * len(plans)
+    errors = []
+    with UploadQueue(env["ctx"], chunk_bytes=256 * 1024, max_chunks=64, max_uploads=48) as q:
+        def worker(idx):
+            try:
+                for i in range(idx, len(plans), 16):
+                    data, cuts = plans[i]
+                    up = q.open()
+                    for a, n in cuts:
+                        assert up.write(data[a:a + n]) == n
+                    mid = up.marshal_text()
+                    results[i] = (up.sums(), mid, up.sums())
+                    up.close()
+            except Exception as e:  # pragma: no cover - reported below
+                errors.append(repr(e))
+        ths = [threading.Thread(target=worker, args=(t,)) for t in range(16)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+    assert not errors, errors
+    for (data, cuts), ((sha, crc), (mt_sha, mt_crc), again) in zip(plans, results):
+        assert sha.hex() == hashlib.sha1(data).hexdigest() and crc == zlib.crc32(data)
+        assert again == (sha, crc)  # Sum is non-destructive
+        o = oracle.Sha1()
+        for a, n in cuts:
+            o.write(data[a:a + n])
+        assert mt_sha.decode() == o.marshal_text()
+        assert mt_crc.decode() == "%08x" % zlib.crc32(data)
+
+
+def test_upload_resume_and_quirks(env, oracle):
+    """Open from a saved .info state (fileinfo.go:29-58), continue, and Go's panic states."""
+    from efes_amd._lib import Sha1State
+    from efes_amd.uploads import UploadQueue
+    with UploadQueue(env["ctx"], chunk_bytes=4096, max_chunks=8, max_uploads=4) as q:
+        first, rest = b"a" * 1000, bytes(range(256)) * 300
+        o = oracle.Sha1()
+        o.write(first)
+        st = Sha1State()
+        st.h[:] = list(o.st.h)
+        st.x[:] = bytes(o.st.x)
+        st.nx, st.len = o.st.nx, o.st.len
+        up = q.open(st, zlib.crc32(first))
+        up.write(rest)
+        sha, crc = up.sums()
+        assert sha.hex() == hashlib.sha1(first + rest).hexdigest() and crc == zlib.crc32(first + rest)
+        up.close()
+        bad = Sha1State()
+        bad.nx = 65
+        up = q.open(bad)
+        with pytest.raises(env["efes"].EfesError) as e:
+            up.write(b"x")
+        assert e.value.code == env["efes"].EFES_ERR_STATE
+        up.close()
+        odd = Sha1State()
+        odd.h[:] = list(o.st.h)
+        odd.nx, odd.len = 3, 0  # nx inconsistent with len: Go's checkSum panics (sha1.go:107-109)
+        up = q.open(odd)
+        with pytest.raises(env["efes"].EfesError) as e:
+            up.sums()
+        assert e.value.code == env["efes"].EFES_ERR_STATE
+        up.close()

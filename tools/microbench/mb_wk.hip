@@ -98,6 +98,40 @@ __global__ __launch_bounds__(64) void kq(const uint32_t* __restrict__ g, uint32_
   if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
 }
 
+// WK from global memory with vector loads (uniform address: one cache line per instruction),
+// next block prefetched into a second register set while the current block runs.
+template <int ALL>
+__global__ __launch_bounds__(64) void kg(const uint32_t* __restrict__ g, uint32_t* out, uint64_t* cyc, int nblocks) {
+  typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+  const __attribute__((address_space(1))) v4u* ring = (const __attribute__((address_space(1))) v4u*)g;
+  uint32_t h[5] = {0x67452301u + blockIdx.x, 0xEFCDAB89u, 0x98BADCFEu, 0x10325476u, 0xC3D2E1F0u};
+  const bool fetch = ALL || (threadIdx.x & 63) == 0;
+  uint32_t vz = 0;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(vz));  // a VGPR zero: keeps the loads on the vector path
+  ring += vz;
+  uint64_t t0 = __builtin_amdgcn_s_memtime();
+  uint4 A[20], B[20];
+  if (fetch) {
+#pragma unroll
+    for (int q = 0; q < 20; ++q) { v4u v = ring[q]; A[q] = make_uint4(v.x, v.y, v.z, v.w); }
+  }
+  for (int b = 0; b < nblocks; b += 2) {
+    if (fetch) {
+#pragma unroll
+      for (int q = 0; q < 20; ++q) { v4u v = ring[((b + 1) & 63) * 20 + q]; B[q] = make_uint4(v.x, v.y, v.z, v.w); }
+    }
+    compress_regs(h, A);
+    if (fetch) {
+#pragma unroll
+      for (int q = 0; q < 20; ++q) { v4u v = ring[((b + 2) & 63) * 20 + q]; A[q] = make_uint4(v.x, v.y, v.z, v.w); }
+    }
+    compress_regs(h, B);
+  }
+  uint64_t t1 = __builtin_amdgcn_s_memtime();
+  out[blockIdx.x * 64 + threadIdx.x] = h[0] ^ h[1] ^ h[2] ^ h[3] ^ h[4];
+  if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
+}
+
 template <int MODE>
 __global__ __launch_bounds__(64) void k(uint32_t* out, uint64_t* cyc, int nblocks) {
   __shared__ __attribute__((aligned(16))) uint4 ring[64][20];
@@ -188,6 +222,6 @@ int main() {
     return 0;
   };
   for (int g : {1, 1024}) { run("regs", k<0>, g); run("lds", k<1>, g); run("pipe", k<2>, g); run("lds16", k<3>, g); run("lds1", k<4>, g); run("pipe1", k<5>, g);
-                            runs("smem4", ks<4>, g); runs("smem64", ks<64>, g); runs("squarter", kq, g); }
+                            runs("smem4", ks<4>, g); runs("smem64", ks<64>, g); runs("squarter", kq, g); runs("gpipe", kg<1>, g); runs("gpipe1", kg<0>, g); }
   return 0;
 }

@@ -58,6 +58,9 @@ def parse_args(argv=None):
     p.add_argument("--host-inclusive", choices=["auto", "on", "off"], default="auto",
                    help="also time the host-resident path (pinned H2D + hash); auto = N=1 only")
     p.add_argument("--segment-bytes", type=int, default=1 << 20, help="host-inclusive pipeline segment")
+    p.add_argument("--dist-backend", default="nccl", help="N>1 timing barrier/max only (no data-path collective)")
+    p.add_argument("--all-ranks-on-device0", action="store_true",
+                   help="rehearse the N>1 path on a 1-GPU box (use with --dist-backend gloo)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="minimum CPU work in the cpu_baseline sample")
     return p.parse_args(argv)
 
@@ -203,15 +206,19 @@ def main(argv=None):
     rank, local, world = env_rank()
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
+    dev_index = 0 if args.all_ranks_on_device0 else local
     dist = None
     if world > 1:
         import torch.distributed as dist
 
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    device = f"cuda:{local}"
-    torch.cuda.set_device(local)
-    ctx = default_context(local)
+        torch.cuda.set_device(dev_index)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
+        else:
+            dist.init_process_group(args.dist_backend)
+    device = f"cuda:{dev_index}"
+    torch.cuda.set_device(dev_index)
+    ctx = default_context(dev_index)
     stream = torch.cuda.Stream(device=device)
     mode = {"auto": MODE_AUTO, "deep": MODE_DEEP, "wide": MODE_WIDE}[args.mode]
 
@@ -240,7 +247,7 @@ def main(argv=None):
     kernel_ms = ev0.elapsed_time(ev1) / max(1, steps)
     for b in batches:
         assert (b.status_host() == 0).all(), "hash jobs reported an error status"
-    wall = max_over_ranks(wall, device)  # the job takes as long as its slowest rank
+    wall = max_over_ranks(wall, device if args.dist_backend == "nccl" else None)  # slowest rank
 
     bytes_timed = sum(step_bytes[k % len(step_bytes)] for k in range(steps))
     value = world * bytes_timed / wall / GiB

@@ -392,10 +392,14 @@ __device__ __forceinline__ uint32_t fin_byte(const uint8_t* xl, uint32_t i, uint
   return 0u;
 }
 
-__device__ __forceinline__ void wide_block(const uint32_t (&le)[16], bool do_sha, bool do_crc,
-                                           const uint32_t (&t)[8][256], uint32_t (&h)[5], uint32_t& crc_raw) {
-  if (do_crc) crc_raw = crc_words_raw(t, crc_raw, le);
-  if (do_sha) {
+// One 64-B block of one lane's message.  kSha/kCrc are wave-uniform (template) so the CRC table
+// lookups and the SHA-1 rounds sit in one basic block and the scheduler can interleave them; a
+// lane that does not need one of the two computes it anyway and never stores it.
+template <bool kSha, bool kCrc>
+__device__ __forceinline__ void wide_block(const uint32_t (&le)[16], const uint32_t (&t)[8][256], uint32_t (&h)[5],
+                                           uint32_t& crc_raw) {
+  if constexpr (kCrc) crc_raw = crc_words_raw(t, crc_raw, le);
+  if constexpr (kSha) {
     uint32_t w[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) w[k] = bswap(le[k]);
@@ -407,18 +411,26 @@ __device__ __forceinline__ void wide_block(const uint32_t (&le)[16], bool do_sha
 // b is compressed (a lone uncoalesced 64-B load per lane would otherwise expose the full
 // memory latency every block).  Lanes run their own trip counts; with jobs sorted by length
 // the lanes of a wave finish together.
-template <bool kAligned16>
-__device__ __forceinline__ void wide_bulk(const uint8_t* q, uint64_t nbulk, bool do_sha, bool do_crc,
-                                          const uint32_t (&t)[8][256], uint32_t (&h)[5], uint32_t& crc_raw) {
+template <bool kAligned16, bool kSha, bool kCrc>
+__device__ __forceinline__ void wide_bulk(const uint8_t* q, uint64_t nbulk, const uint32_t (&t)[8][256],
+                                          uint32_t (&h)[5], uint32_t& crc_raw) {
   uint32_t A[16], B[16];
   if (nbulk) load_block_le<kAligned16>(q, A);
   for (uint64_t b = 0; b < nbulk; b += 2) {
     if (b + 1 < nbulk) load_block_le<kAligned16>(q + 64 * (b + 1), B);
-    wide_block(A, do_sha, do_crc, t, h, crc_raw);
+    wide_block<kSha, kCrc>(A, t, h, crc_raw);
     if (b + 1 >= nbulk) break;
     if (b + 2 < nbulk) load_block_le<kAligned16>(q + 64 * (b + 2), A);
-    wide_block(B, do_sha, do_crc, t, h, crc_raw);
+    wide_block<kSha, kCrc>(B, t, h, crc_raw);
   }
+}
+
+template <bool kAligned16>
+__device__ __forceinline__ void wide_bulk_any(const uint8_t* q, uint64_t nbulk, bool any_sha, bool any_crc,
+                                              const uint32_t (&t)[8][256], uint32_t (&h)[5], uint32_t& crc_raw) {
+  if (any_sha && any_crc) wide_bulk<kAligned16, true, true>(q, nbulk, t, h, crc_raw);
+  else if (any_sha) wide_bulk<kAligned16, true, false>(q, nbulk, t, h, crc_raw);
+  else if (any_crc) wide_bulk<kAligned16, false, true>(q, nbulk, t, h, crc_raw);
 }
 
 __global__ __launch_bounds__(64 * kWideWaves, 2) void wide_kernel(const efes_job* __restrict__ jobs, uint32_t njobs,
@@ -490,8 +502,9 @@ __global__ __launch_bounds__(64 * kWideWaves, 2) void wide_kernel(const efes_job
   const uint8_t* q = p + pos;
   const uint64_t nbulk = go ? (plen - pos) >> 6 : 0;
   const bool all16 = __all(!go || (reinterpret_cast<uintptr_t>(q) & 15) == 0);
-  if (all16) wide_bulk<true>(q, nbulk, do_sha, do_crc, L.slice8, h, crc_raw);
-  else wide_bulk<false>(q, nbulk, do_sha, do_crc, L.slice8, h, crc_raw);
+  const bool any_sha = __any(do_sha), any_crc = __any(do_crc);  // wave-uniform
+  if (all16) wide_bulk_any<true>(q, nbulk, any_sha, any_crc, L.slice8, h, crc_raw);
+  else wide_bulk_any<false>(q, nbulk, any_sha, any_crc, L.slice8, h, crc_raw);
 
   // ---- tail
   const uint64_t tpos = pos + (nbulk << 6);

@@ -44,10 +44,18 @@ def parse_args(argv=None):
     p.add_argument("--chunks", type=int, default=1024, help="chunks per GPU")
     p.add_argument("--chunk-bytes", type=int, default=4 << 20)
     p.add_argument("--mode", choices=["auto", "deep", "wide"], default="auto")
-    p.add_argument("--workload", choices=["chunks4m", "mixed", "ingest"], default="chunks4m",
+    p.add_argument("--workload", choices=["chunks4m", "mixed", "ingest", "uploads"], default="chunks4m",
                    help="chunks4m = BASELINE configs[1]/[2] (the metric); mixed = configs[3]; ingest = configs[4]")
     p.add_argument("--pool-gib", type=int, default=64, help="device pool aliased by mixed/ingest chunks")
     p.add_argument("--mixed-chunks", type=int, default=65536)
+    p.add_argument("--mixed-launches", type=int, default=1,
+                   help="deal the longest-first mixed job list round-robin into this many launches")
+    p.add_argument("--upload-threads", type=int, default=16)
+    p.add_argument("--uploads", type=int, default=1024)
+    p.add_argument("--upload-bytes", type=int, default=4 << 20)
+    p.add_argument("--write-bytes", type=int, default=32 << 10, help="io.Copy buffer size (32 KiB)")
+    p.add_argument("--progress", action="store_true",
+                   help="synchronize after every step and print progress to stderr (long workloads)")
     p.add_argument("--ingest-tib", type=float, default=10.0)
     p.add_argument("--ingest-scale", type=float, default=1.0)
     p.add_argument("--ingest-batch", type=int, default=65536)
@@ -135,6 +143,49 @@ def host_inclusive(ctx, data, n: int, chunk: int, do_crc: bool, segment: int, ba
             "note": "pinned host chunks -> hipMemcpyAsync H2D (copy stream) overlapped with hashing; not `value`"}
 
 
+def uploads_workload(args, ctx):
+    """Concurrent uploads through the batching dispatcher (efes_queue): --upload-threads threads
+    each run uploads of --upload-bytes as Write calls of --write-bytes (io.Copy's 32 KiB,
+    filereceiver.go:209) from pageable host memory, then Sum -- the server path end to end
+    (host staging, H2D, hashing, sync point).  Returns the result dict (not the metric)."""
+    import hashlib
+    import threading
+    import zlib
+
+    import numpy as np
+
+    from efes_amd.uploads import UploadQueue
+
+    rng = np.random.default_rng(5)
+    src = rng.integers(0, 256, args.upload_bytes, dtype=np.uint8).tobytes()
+    want = (hashlib.sha1(src).digest(), zlib.crc32(src))
+    T, U, S, W = args.upload_threads, args.uploads, args.upload_bytes, args.write_bytes
+    bad = []
+    q = UploadQueue(ctx, chunk_bytes=1 << 20, max_chunks=max(64, 4 * T), max_uploads=T)
+
+    def worker(t):
+        mv = memoryview(src)
+        for _ in range(t, U, T):
+            up = q.open()
+            for a in range(0, S, W):
+                up.write(mv[a:a + W])
+            if up.sums() != want:
+                bad.append(t)
+            up.close()
+
+    t0 = time.perf_counter()
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(T)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    wall = time.perf_counter() - t0
+    q.close()
+    return {"value": round(U * S / wall / GiB, 3), "unit": "GiB/s", "uploads": U, "upload_bytes": S,
+            "write_bytes": W, "threads": T, "seconds": round(wall, 3), "digests_match": not bad,
+            "note": "pageable host Writes -> pinned staging -> batched launches -> per-upload Sum"}
+
+
 def make_workload(args, rank: int, world: int, ctx, device: str, stream):
     """Device-resident inputs + the job batches of one workload.
 
@@ -174,11 +225,12 @@ def make_workload(args, rank: int, world: int, ctx, device: str, stream):
         sizes = np.asarray(MIXED_CLASSES, dtype=np.uint64)[rng.integers(0, len(MIXED_CLASSES), args.mixed_chunks)]
         sizes = np.sort(sizes)[::-1].copy()  # longest first: equal lengths per wave, LPT tail
         offs = (rng.integers(0, (pool - sizes.astype(np.int64)) // 256 + 1) * 256).astype(np.uint64)
-        b = DeviceBatch(data.data_ptr(), offs, sizes, **kw)
+        L = max(1, args.mixed_launches)
+        batches = [DeviceBatch(data.data_ptr(), offs[k::L], sizes[k::L], **kw) for k in range(L)]
         total = int(sizes.sum())
-        return data, [b], [total], {"workload": f"mixed ChunkSize 64K..64M x {args.mixed_chunks} chunks "
-                                                "(BASELINE configs[3])", "chunks_per_gpu": args.mixed_chunks,
-                                    "bytes_per_gpu": total, "pool_bytes": pool}
+        return data, batches, [int(sizes[k::L].sum()) for k in range(L)], {
+            "workload": f"mixed ChunkSize 64K..64M x {args.mixed_chunks} chunks (BASELINE configs[3])",
+            "chunks_per_gpu": args.mixed_chunks, "bytes_per_gpu": total, "pool_bytes": pool, "launches": L}
     chunk = 4 << 20
     per_gpu = int(round(args.ingest_tib * (1 << 40) / chunk / 8 * args.ingest_scale))
     slots = pool // chunk
@@ -222,6 +274,14 @@ def main(argv=None):
     stream = torch.cuda.Stream(device=device)
     mode = {"auto": MODE_AUTO, "deep": MODE_DEEP, "wide": MODE_WIDE}[args.mode]
 
+    if args.workload == "uploads":
+        res = uploads_workload(args, ctx)
+        if rank == 0:
+            print(json.dumps({"metric": "GiB/s hashed through concurrent uploads (efes_queue), host-resident",
+                              "workload": "uploads", **res}), flush=True)
+        if dist:
+            dist.destroy_process_group()
+        return
     with torch.cuda.stream(stream):
         data, batches, step_bytes, config = make_workload(args, rank, world, ctx, device, stream)
         steps = args.steps if len(batches) == 1 else len(batches)
@@ -239,6 +299,10 @@ def main(argv=None):
         ev0.record(stream)
         for k in range(steps):
             batches[k % len(batches)].submit(mode)
+            if args.progress:
+                torch.cuda.synchronize(device)
+                print(f"[bench] step {k + 1}/{steps} done at {time.perf_counter() - t0:.1f} s", file=sys.stderr,
+                      flush=True)
         ev1.record(stream)
         torch.cuda.synchronize(device)
         if dist:

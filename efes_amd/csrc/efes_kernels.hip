@@ -392,36 +392,39 @@ __device__ __forceinline__ uint32_t fin_byte(const uint8_t* xl, uint32_t i, uint
   return 0u;
 }
 
-// One 64-B block of one lane's message.  kSha/kCrc are wave-uniform (template) so the CRC table
-// lookups and the SHA-1 rounds sit in one basic block and the scheduler can interleave them; a
-// lane that does not need one of the two computes it anyway and never stores it.
-template <bool kSha, bool kCrc>
-__device__ __forceinline__ void wide_block(const uint32_t (&le)[16], const uint32_t (&t)[8][256], uint32_t (&h)[5],
-                                           uint32_t& crc_raw) {
-  if constexpr (kCrc) crc_raw = crc_words_raw(t, crc_raw, le);
-  if constexpr (kSha) {
-    uint32_t w[16];
+__device__ __forceinline__ void sha_block(const uint32_t (&le)[16], uint32_t (&h)[5]) {
+  uint32_t w[16];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) w[k] = bswap(le[k]);
-    compress_inline(h, w);
-  }
+  for (int k = 0; k < 16; ++k) w[k] = bswap(le[k]);
+  compress_inline(h, w);
 }
 
-// Whole blocks of one lane's message, software-pipelined: block b+1 is in flight while block
-// b is compressed (a lone uncoalesced 64-B load per lane would otherwise expose the full
-// memory latency every block).  Lanes run their own trip counts; with jobs sorted by length
-// the lanes of a wave finish together.
+// Whole blocks of one lane's message, software-pipelined: the next block is in flight while
+// the current one is compressed (a lone uncoalesced 64-B load per lane would otherwise expose
+// the full memory latency every block).  kSha/kCrc are wave-uniform template flags, so CRC
+// lookups and SHA-1 rounds share one basic block; a lane that needs only one of the two
+// computes both and never stores the other.  Lanes run their own trip counts; with jobs
+// sorted by length the lanes of a wave finish together.
 template <bool kAligned16, bool kSha, bool kCrc>
 __device__ __forceinline__ void wide_bulk(const uint8_t* q, uint64_t nbulk, const uint32_t (&t)[8][256],
                                           uint32_t (&h)[5], uint32_t& crc_raw) {
+  // Skewed: each step compresses block b and CRCs block b+1, two chains with no data
+  // dependence on each other, so a lone wave (configs 3/4 run 1-2 waves per SIMD) has
+  // independent work to issue while either chain waits on its latency.
   uint32_t A[16], B[16];
-  if (nbulk) load_block_le<kAligned16>(q, A);
+  if (nbulk == 0) return;
+  load_block_le<kAligned16>(q, A);
+  if (nbulk > 1) load_block_le<kAligned16>(q + 64, B);
+  if constexpr (kCrc) crc_raw = crc_words_raw(t, crc_raw, A);
   for (uint64_t b = 0; b < nbulk; b += 2) {
-    if (b + 1 < nbulk) load_block_le<kAligned16>(q + 64 * (b + 1), B);
-    wide_block<kSha, kCrc>(A, t, h, crc_raw);
+    if constexpr (kSha) sha_block(A, h);
     if (b + 1 >= nbulk) break;
+    if constexpr (kCrc) crc_raw = crc_words_raw(t, crc_raw, B);
     if (b + 2 < nbulk) load_block_le<kAligned16>(q + 64 * (b + 2), A);
-    wide_block<kSha, kCrc>(B, t, h, crc_raw);
+    if constexpr (kSha) sha_block(B, h);
+    if (b + 2 >= nbulk) break;
+    if constexpr (kCrc) crc_raw = crc_words_raw(t, crc_raw, A);
+    if (b + 3 < nbulk) load_block_le<kAligned16>(q + 64 * (b + 3), B);
   }
 }
 

@@ -545,3 +545,99 @@ def test_upload_resume_and_quirks(env, oracle):
             up.sums()
         assert e.value.code == env["efes"].EFES_ERR_STATE
         up.close()
+
+
+def test_host_ingest_many_jobs_wide_path(env, oracle):
+    """> 1536 jobs per segment: AUTO picks the lane-per-job kernel for the host pipeline too."""
+    from efes_amd.batch import HostBatch
+    rng = np.random.default_rng(31)
+    n = 2500
+    lengths = rng.integers(0, 9000, n)
+    offsets = np.concatenate([[0], np.cumsum(lengths)[:-1]]).astype(np.uint64)
+    host = oracle.fill_synthetic(int(lengths.sum()) + 8, 4321)
+    hb = HostBatch(host.ctypes.data, offsets, lengths, ctx=env["ctx"])
+    hb.run(4096)
+    assert (hb.status[:n] == 0).all()
+    for i in range(0, n, 11):
+        d = host[int(offsets[i]):int(offsets[i]) + int(lengths[i])].tobytes()
+        assert hb.sha1_hex()[i] == hashlib.sha1(d).hexdigest() and int(hb.crc_sum()[i]) == zlib.crc32(d)
+
+
+def test_deep_mode_more_jobs_than_resident_waves(env, oracle):
+    """DEEP with 3000 jobs: more workgroups than fit at once (one per CU by LDS)."""
+    rng = np.random.default_rng(8)
+    n = 3000
+    lengths = rng.integers(0, 20000, n)
+    offsets = np.concatenate([[0], np.cumsum(lengths)[:-1]]).astype(np.uint64)
+    host = oracle.fill_synthetic(int(lengths.sum()) + 8, 99)
+    buf = device_buffer(env, host)
+    b = env["DeviceBatch"](buf.data_ptr(), offsets, lengths, fresh=True, ctx=env["ctx"])
+    b.run(env["efes"].MODE_DEEP)
+    assert (b.status_host() == 0).all()
+    shas, crcs = b.sha1_hex(), b.crc_sum()
+    for i in range(0, n, 13):
+        d = host[int(offsets[i]):int(offsets[i]) + int(lengths[i])].tobytes()
+        assert shas[i] == hashlib.sha1(d).hexdigest() and crcs[i] == zlib.crc32(d)
+
+
+def test_upload_midstream_state_then_continue(env, oracle):
+    """.info save in the middle of an upload (filereceiver.go:226), then more PATCH bytes."""
+    from efes_amd.uploads import UploadQueue
+    data = oracle.fill_synthetic(3 * 100_000 + 17, 55).tobytes()
+    with UploadQueue(env["ctx"], chunk_bytes=8192, max_chunks=16, max_uploads=2) as q:
+        up = q.open()
+        o = oracle.Sha1()
+        for a in range(0, 100_000, 32 * 1024):
+            piece = data[a:min(a + 32 * 1024, 100_000)]
+            up.write(piece)
+            o.write(piece)
+        st, crc = up.state()
+        mt, _ = up.marshal_text()
+        assert mt.decode() == o.marshal_text() and crc == zlib.crc32(data[:100_000])
+        up.write(data[100_000:])
+        sha, crc2 = up.sums()
+        assert sha == hashlib.sha1(data).digest() and crc2 == zlib.crc32(data)
+        up.close()
+        # a second upload resumed from the exported state gives the same result
+        up2 = q.open(st, crc)
+        up2.write(data[100_000:])
+        assert up2.sums() == (sha, crc2)
+        up2.close()
+
+
+def test_upload_queue_limits(env):
+    from efes_amd.uploads import UploadQueue
+    efes = env["efes"]
+    with pytest.raises(efes.EfesError):
+        UploadQueue(env["ctx"], chunk_bytes=4096, max_chunks=4, max_uploads=4)  # needs max_uploads < max_chunks
+    with UploadQueue(env["ctx"], chunk_bytes=4096, max_chunks=4, max_uploads=2) as q:
+        a, b = q.open(), q.open()
+        with pytest.raises(efes.EfesError) as e:
+            q.open()
+        assert e.value.code == efes.EFES_ERR_NOMEM
+        # back-pressure: more bytes than the staging pool holds, from one upload
+        blob = bytes(range(256)) * 200
+        for _ in range(5):
+            a.write(blob)
+        assert a.sums()[0] == hashlib.sha1(blob * 5).digest()
+        a.close()
+        b.close()
+
+
+def test_bench_emits_driver_json(env):
+    """bench.py's contract keys on a tiny configuration (the driver parses this line)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--chunks", "16", "--chunk-bytes", "65536",
+                          "--steps", "2", "--warmup", "1", "--cpu-seconds", "0.1", "--segment-bytes", "16384"],
+                         capture_output=True, text=True, timeout=600, check=True).stdout
+    d = json.loads(out.strip().splitlines()[-1])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in d, k
+    assert d["steps"] == 2 and d["n_gpus"] == 1 and d["value"] > 0
+    assert d["roofline"]["bound"] == "hbm" and 0 < d["roofline"]["frac"] < 1
+    assert d["cpu_baseline"]["digests_match_gpu"] and d["host_inclusive"]["digests_match_device_path"]

@@ -3,8 +3,6 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include <mutex>
-
 #include "../../include/efes_hash.h"
 
 namespace efes {
@@ -56,5 +54,4 @@ struct efes_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   efes::Tables* d_tabs = nullptr;
-  std::mutex mu;
 };

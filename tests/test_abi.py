@@ -135,3 +135,14 @@ def test_crc32_combine_matches_concatenation(efes_lib):
     left = L.efes_crc32_combine(L.efes_crc32_combine(ca, cb, lb), cc, lc)
     right = L.efes_crc32_combine(ca, L.efes_crc32_combine(cb, cc, lc), lb + lc)
     assert left == right
+
+
+def test_integration_doc_binds_only_declared_symbols():
+    """The cgo binding in INTEGRATION.md only calls entry points include/efes_hash.h declares."""
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    used = set(re.findall(r"\bC\.(efes_\w+)\s*\(", doc))
+    assert len(used) >= 15
+    missing = sorted(used - set(declared_functions()))
+    assert not missing, missing
+    for const in set(re.findall(r"\bC\.(EFES_\w+)", doc)):
+        assert re.search(r"#define\s+%s\b" % const, open(HEADER).read()), const

@@ -67,6 +67,8 @@ def parse_args(argv=None):
     p.add_argument("--host-inclusive", choices=["auto", "on", "off"], default="auto",
                    help="also time the host-resident path (pinned H2D + hash); auto = N=1 only")
     p.add_argument("--segment-bytes", type=int, default=1 << 20, help="host-inclusive pipeline segment")
+    p.add_argument("--ingest-leg", choices=["auto", "on", "off"], default="auto",
+                   help="also report BASELINE configs[4] per-GPU (auto = N=1 only)")
     p.add_argument("--dist-backend", default="nccl", help="N>1 timing barrier/max only (no data-path collective)")
     p.add_argument("--all-ranks-on-device0", action="store_true",
                    help="rehearse the N>1 path on a 1-GPU box (use with --dist-backend gloo)")
@@ -238,6 +240,63 @@ def make_workload(args, rank: int, world: int, ctx, device: str, stream):
                                    "launches": len(batches)}
 
 
+def run_timed(batches, steps: int, warmup: int, mode: int, device: str, stream, dist, progress: bool = False):
+    """W untimed warm-up launches, then exactly `steps` launches bracketed by barrier +
+    synchronize; returns (wall seconds of this rank, average kernel ms from HIP events recorded
+    on the launch stream)."""
+    import torch
+
+    for _ in range(warmup):
+        batches[0].submit(mode)
+    torch.cuda.synchronize(device)
+    if warmup:
+        assert (batches[0].status_host() == 0).all(), "hash jobs reported an error status"
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for k in range(steps):
+        batches[k % len(batches)].submit(mode)
+        if progress:
+            torch.cuda.synchronize(device)
+            print(f"[bench] step {k + 1}/{steps} done at {time.perf_counter() - t0:.1f} s", file=sys.stderr,
+                  flush=True)
+    ev1.record(stream)
+    torch.cuda.synchronize(device)
+    if dist:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    for b in batches:
+        assert (b.status_host() == 0).all(), "hash jobs reported an error status"
+    return wall, ev0.elapsed_time(ev1) / max(1, steps)
+
+
+def ingest_leg(args, rank: int, world: int, ctx, device: str, stream, mode: int):
+    """BASELINE configs[4] beside the metric: this GPU's share of a 10 TiB ingest of 4 MiB
+    chunks (327 680 chunks, per-GPU queue) in launches of 131 072 chunks aliasing a 64 GiB pool."""
+    import argparse as _ap
+
+    import torch
+
+    a = _ap.Namespace(**vars(args))
+    a.workload, a.ingest_batch, a.ingest_scale = "ingest", 131072, args.ingest_scale
+    with torch.cuda.stream(stream):
+        data, batches, step_bytes, config = make_workload(a, rank, world, ctx, device, stream)
+        wall, kernel_ms = run_timed(batches, len(batches), 1, mode, device, stream, None)
+    total = sum(step_bytes)
+    per_launch = total / len(batches)
+    achieved = per_launch / (kernel_ms * 1e-3) / 1e9
+    del data, batches
+    torch.cuda.empty_cache()
+    return {"value": round(total / wall / GiB, 3), "unit": "GiB/s", "workload": config["workload"],
+            "chunks": config["chunks_per_gpu"], "launches": config["launches"], "kernel": "wide_kernel",
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBPS, 5), "kernel_ms": round(kernel_ms, 3)},
+            "note": "many concurrent chunks per GPU (configs[4] per-GPU queue); not `value`"}
+
+
 def main(argv=None):
     args = parse_args(argv)
     import torch
@@ -277,32 +336,7 @@ def main(argv=None):
     with torch.cuda.stream(stream):
         data, batches, step_bytes, config = make_workload(args, rank, world, ctx, device, stream)
         steps = args.steps if len(batches) == 1 else len(batches)
-        for _ in range(args.warmup):
-            batches[0].submit(mode)
-        torch.cuda.synchronize(device)
-        if args.warmup:
-            assert (batches[0].status_host() == 0).all(), "hash jobs reported an error status"
-
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        if dist:
-            dist.barrier()
-        torch.cuda.synchronize(device)
-        t0 = time.perf_counter()
-        ev0.record(stream)
-        for k in range(steps):
-            batches[k % len(batches)].submit(mode)
-            if args.progress:
-                torch.cuda.synchronize(device)
-                print(f"[bench] step {k + 1}/{steps} done at {time.perf_counter() - t0:.1f} s", file=sys.stderr,
-                      flush=True)
-        ev1.record(stream)
-        torch.cuda.synchronize(device)
-        if dist:
-            dist.barrier()
-        wall = time.perf_counter() - t0
-    kernel_ms = ev0.elapsed_time(ev1) / max(1, steps)
-    for b in batches:
-        assert (b.status_host() == 0).all(), "hash jobs reported an error status"
+        wall, kernel_ms = run_timed(batches, steps, args.warmup, mode, device, stream, dist, args.progress)
     wall = max_over_ranks(wall, device if args.dist_backend == "nccl" else None)  # slowest rank
 
     bytes_timed = sum(step_bytes[k % len(step_bytes)] for k in range(steps))
@@ -347,6 +381,8 @@ def main(argv=None):
         if args.host_inclusive == "on" or (args.host_inclusive == "auto" and world == 1):
             out["host_inclusive"] = host_inclusive(ctx, data, n, chunk, not args.sha1_only, args.segment_bytes,
                                                    batches[0])
+        if args.ingest_leg == "on" or (args.ingest_leg == "auto" and world == 1):
+            out["ingest_config"] = ingest_leg(args, rank, world, ctx, device, stream, MODE_AUTO)
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             threads = args.cpu_threads or host_threads()
             out["cpu_baseline"] = cpu_baseline(batches[0], data, min(n, args.cpu_max_chunks), chunk, threads,

@@ -57,8 +57,10 @@ __device__ __forceinline__ uint32_t crc_words_raw(const uint32_t (&t)[8][256], u
   for (int s = 0; s < 8; ++s) {
     const uint32_t hi = le[2 * s + 1];
     crc ^= le[2 * s];
-    crc = t[0][hi >> 24] ^ t[1][(hi >> 16) & 0xffu] ^ t[2][(hi >> 8) & 0xffu] ^ t[3][hi & 0xffu] ^
-          t[4][crc >> 24] ^ t[5][(crc >> 16) & 0xffu] ^ t[6][(crc >> 8) & 0xffu] ^ t[7][crc & 0xffu];
+    // eight lookups folded with three-input XORs (v_bitop3_b32 0x96): 4 VALU instead of 7
+    const uint32_t a = __builtin_amdgcn_bitop3_b32(t[0][hi >> 24], t[1][(hi >> 16) & 0xffu], t[2][(hi >> 8) & 0xffu], 0x96);
+    const uint32_t b = __builtin_amdgcn_bitop3_b32(t[3][hi & 0xffu], t[4][crc >> 24], t[5][(crc >> 16) & 0xffu], 0x96);
+    crc = __builtin_amdgcn_bitop3_b32(a, b, t[6][(crc >> 8) & 0xffu] ^ t[7][crc & 0xffu], 0x96);
   }
   return crc;
 }

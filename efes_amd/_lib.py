@@ -28,6 +28,7 @@ EFES_ERR_DEVICE_FAULT = -7
 
 EFES_JOB_FINALIZE = 0x1
 EFES_JOB_INIT = 0x2
+EFES_HASH_SHA1, EFES_HASH_CRC32 = 0x1, 0x2
 MODE_AUTO, MODE_DEEP, MODE_WIDE = 0, 1, 2
 kAutoDeepMaxJobs = 1536  # efes_internal.hpp: AUTO picks DEEP up to this many jobs
 
@@ -85,7 +86,7 @@ SIGNATURES = {
     "efes_host_free": (_I, [_VP, _VP]),
     "efes_queue_create": (_I, [_VP, _U64, _U32, _U32, _P(_VP)]),
     "efes_queue_destroy": (None, [_VP]),
-    "efes_upload_open": (_I, [_VP, _P(Sha1State), _P(Crc32State), _P(_VP)]),
+    "efes_upload_open": (_I, [_VP, _U32, _P(Sha1State), _P(Crc32State), _P(_VP)]),
     "efes_upload_write": (_I, [_VP, _VP, _S]),
     "efes_upload_flush": (_I, [_VP]),
     "efes_upload_state": (_I, [_VP, _P(Sha1State), _P(Crc32State)]),

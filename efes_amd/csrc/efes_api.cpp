@@ -1,13 +1,8 @@
-// efes_api.cpp -- C ABI of libefeshash (include/efes_hash.h).
-//
-// Layer 1 (efes_hash_submit) enqueues the gfx950 kernels of efes_kernels.hip.
-// Layer 2 (efes_sha1_* / efes_crc32_*) mirrors the Go digests the reference streams
-// uploads through: sha1digest (sha1.go:29-120, sha1_efes.go:25-64) and crc32digest
-// (crc32.go:48-93, crc32_efes.go:18-40).  A streaming object stages the bytes of its
-// Write calls and hashes them on the GPU in one job at the next Sum/MarshalText (or
-// when the staging exceeds kFlushBytes).  Host code never compresses a block: it only
-// replays Go's byte bookkeeping of the tail buffer (x, nx, len), so the device state
-// plus that bookkeeping reproduces Go's state exactly, stale x bytes included.
+// efes_api.cpp -- C ABI of libefeshash (include/efes_hash.h): contexts, the batched
+// device-resident submit (layer 1, kernels in efes_kernels.hip), device-memory helpers,
+// the CRC tables, CRC combine, and the text codecs of sha1_efes.go / crc32_efes.go.
+// Host-resident ingest is efes_ingest.cpp, the upload dispatcher efes_queue.cpp, and the
+// Go-surface streaming digests efes_stream.cpp.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -23,8 +18,6 @@ using efes::Tables;
 
 
 namespace {
-
-constexpr size_t kFlushBytes = 64u << 20;
 
 int hip_err(hipError_t e) { return e == hipSuccess ? EFES_OK : EFES_ERR_HIP; }
 
@@ -76,85 +69,6 @@ void put_be64(uint8_t* b, uint64_t v) { for (int i = 0; i < 8; ++i) b[i] = (uint
 uint32_t get_be32(const uint8_t* b) { return (uint32_t)b[0] << 24 | (uint32_t)b[1] << 16 | (uint32_t)b[2] << 8 | b[3]; }
 uint64_t get_be64(const uint8_t* b) { uint64_t v = 0; for (int i = 0; i < 8; ++i) v = v << 8 | b[i]; return v; }
 
-// Device scratch of one streaming object: [job 56 | pad | sha1 state 104 | crc 4 | sum 24 | status 4].
-struct DevScratch {
-  uint8_t* base = nullptr;
-  uint8_t* data = nullptr;
-  size_t cap = 0;
-  efes_job* job() { return reinterpret_cast<efes_job*>(base); }
-  efes_sha1_state* sha1() { return reinterpret_cast<efes_sha1_state*>(base + 64); }
-  efes_crc32_state* crc() { return reinterpret_cast<efes_crc32_state*>(base + 64 + 104); }
-  uint8_t* sum() { return base + 64 + 104 + 8; }
-  int32_t* status() { return reinterpret_cast<int32_t*>(base + 64 + 104 + 8 + 24); }
-  static constexpr size_t kBytes = 256;
-};
-
-struct Staged {
-  efes_ctx* ctx = nullptr;
-  std::vector<uint8_t> pending;
-  DevScratch dev;
-  int latched = EFES_OK;
-
-  int ensure(size_t need) {
-    DeviceGuard g(ctx->device);
-    if (!dev.base && hipMalloc(reinterpret_cast<void**>(&dev.base), DevScratch::kBytes) != hipSuccess) return EFES_ERR_HIP;
-    if (need > dev.cap) {
-      if (dev.data) (void)hipFree(dev.data);
-      dev.data = nullptr;
-      dev.cap = 0;
-      size_t cap = 1 << 16;
-      while (cap < need) cap <<= 1;
-      if (hipMalloc(reinterpret_cast<void**>(&dev.data), cap) != hipSuccess) return EFES_ERR_HIP;
-      dev.cap = cap;
-    }
-    return EFES_OK;
-  }
-  void release() {
-    DeviceGuard g(ctx->device);
-    if (dev.data) (void)hipFree(dev.data);
-    if (dev.base) (void)hipFree(dev.base);
-    dev = DevScratch{};
-  }
-  // Runs one job over `pending` with the given in-states; copies states (and sum) back.
-  int run(efes_sha1_state* sha1, efes_crc32_state* crc, bool finalize, uint8_t sum_out[24]) {
-    const size_t n = pending.size();
-    int rc = ensure(n ? n : 1);
-    if (rc) return rc;
-    DeviceGuard g(ctx->device);
-    hipStream_t s = ctx->stream;
-    efes_job job{};
-    job.data = dev.data;
-    job.length = n;
-    job.sha1 = sha1 ? dev.sha1() : nullptr;
-    job.crc32 = crc ? dev.crc() : nullptr;
-    job.sum = finalize ? dev.sum() : nullptr;
-    job.status = dev.status();
-    job.flags = finalize ? EFES_JOB_FINALIZE : 0u;
-    uint8_t host[DevScratch::kBytes] = {};
-    memcpy(host, &job, sizeof job);
-    if (sha1) memcpy(host + 64, sha1, sizeof *sha1);
-    if (crc) memcpy(host + 64 + 104, crc, sizeof *crc);
-    hipError_t e = hipMemcpyAsync(dev.base, host, sizeof host, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess && n) e = hipMemcpyAsync(dev.data, pending.data(), n, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess) e = efes::launch_deep(dev.job(), 1, ctx->d_tabs, s);
-    if (e == hipSuccess) e = hipMemcpyAsync(host, dev.base, sizeof host, hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipStreamSynchronize(s);
-    if (e != hipSuccess) return latched = EFES_ERR_HIP;
-    int32_t status;
-    memcpy(&status, host + 64 + 104 + 8 + 24, 4);
-    if (status != EFES_OK && status != EFES_ERR_STATE) return latched = EFES_ERR_DEVICE_FAULT;
-    if (sha1) {
-      efes_sha1_state out;
-      memcpy(&out, host + 64, sizeof out);
-      memcpy(sha1->h, out.h, sizeof out.h);  // x/nx/len come from the host replay
-    }
-    if (crc) memcpy(crc, host + 64 + 104, sizeof *crc);
-    if (sum_out) memcpy(sum_out, host + 64 + 104 + 8, 24);
-    pending.clear();
-    return status;
-  }
-};
-
 }  // namespace
 
 namespace efes {
@@ -182,17 +96,6 @@ int replay_write(efes_sha1_state* s, const uint8_t* p, size_t n) {
 }
 }  // namespace efes
 using efes::replay_write;
-
-struct efes_sha1 {
-  Staged stg;
-  efes_sha1_state base{};    // state as of the last device flush (h authoritative)
-  efes_sha1_state shadow{};  // Go's x/nx/len after every Write so far
-};
-
-struct efes_crc32 {
-  Staged stg;
-  efes_crc32_state st{};
-};
 
 // ======================================================================= tables
 void efes::build_tables(Tables* t) {
@@ -279,6 +182,7 @@ int efes_ctx_create(int device, efes_ctx** out) {
 
 void efes_ctx_destroy(efes_ctx* ctx) {
   if (!ctx) return;
+  if (ctx->digests) efes_queue_destroy(ctx->digests);  // free the context's digests first
   {
     DeviceGuard g(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
@@ -414,184 +318,6 @@ int efes_crc32_state_unmarshal_text(efes_crc32_state* s, const char* text, size_
   uint8_t b[4];
   if (!hex_decode(b, text, 4)) return EFES_ERR_INVALID_DIGEST;
   s->crc = get_be32(b);
-  return EFES_OK;
-}
-
-// ---- streaming SHA-1 -----------------------------------------------------------------------
-static int sha1_alloc(efes_ctx* ctx, efes_sha1** out, bool reset) {
-  if (!ctx || !out) return EFES_ERR_ARG;
-  efes_sha1* d = new (std::nothrow) efes_sha1;
-  if (!d) return EFES_ERR_NOMEM;
-  d->stg.ctx = ctx;
-  memset(&d->base, 0, sizeof d->base);
-  if (reset) efes_sha1_state_init(&d->base);
-  d->shadow = d->base;
-  *out = d;
-  return EFES_OK;
-}
-
-int efes_sha1_new(efes_ctx* ctx, efes_sha1** out) { return sha1_alloc(ctx, out, true); }
-int efes_sha1_new_zero(efes_ctx* ctx, efes_sha1** out) { return sha1_alloc(ctx, out, false); }
-
-void efes_sha1_free(efes_sha1* d) {
-  if (!d) return;
-  d->stg.release();
-  delete d;
-}
-
-void efes_sha1_reset(efes_sha1* d) {
-  if (!d) return;
-  d->stg.pending.clear();
-  efes_sha1_state_init(&d->base);  // Go's Reset leaves x as it is
-  memcpy(d->base.x, d->shadow.x, 64);
-  d->shadow = d->base;
-}
-
-int efes_sha1_size(void) { return 20; }
-int efes_sha1_block_size(void) { return 64; }
-
-static int sha1_flush(efes_sha1* d, bool finalize, uint8_t sum[24]) {
-  if (d->stg.latched) return d->stg.latched;
-  if (d->stg.pending.empty() && !finalize) return EFES_OK;
-  efes_sha1_state st = d->base;
-  const int rc = d->stg.run(&st, nullptr, finalize, sum);
-  if (rc != EFES_OK && rc != EFES_ERR_STATE) return rc;
-  memcpy(d->shadow.h, st.h, sizeof st.h);  // x/nx/len: the replay is authoritative
-  d->base = d->shadow;
-  return rc;
-}
-
-int efes_sha1_write(efes_sha1* d, const void* p, size_t n) {
-  if (!d || (!p && n)) return EFES_ERR_ARG;
-  if (d->stg.latched) return d->stg.latched;
-  const int rc = replay_write(&d->shadow, static_cast<const uint8_t*>(p), n);
-  if (rc) return rc;
-  try {
-    d->stg.pending.insert(d->stg.pending.end(), static_cast<const uint8_t*>(p), static_cast<const uint8_t*>(p) + n);
-  } catch (...) {
-    return EFES_ERR_NOMEM;
-  }
-  if (d->stg.pending.size() >= kFlushBytes) return sha1_flush(d, false, nullptr);
-  return EFES_OK;
-}
-
-int efes_sha1_sum(efes_sha1* d, uint8_t out[20]) {
-  if (!d || !out) return EFES_ERR_ARG;
-  uint8_t sum[24];
-  const int rc = sha1_flush(d, true, sum);
-  if (rc) return rc;
-  memcpy(out, sum, 20);
-  return EFES_OK;
-}
-
-int efes_sha1_marshal_text(efes_sha1* d, char out[200]) {
-  if (!d || !out) return EFES_ERR_ARG;
-  const int rc = sha1_flush(d, false, nullptr);
-  if (rc) return rc;
-  efes_sha1_state_marshal_text(&d->base, out);
-  return EFES_OK;
-}
-
-int efes_sha1_unmarshal_text(efes_sha1* d, const char* text, size_t n) {
-  if (!d) return EFES_ERR_ARG;
-  efes_sha1_state s;
-  const int rc = efes_sha1_state_unmarshal_text(&s, text, n);
-  if (rc) return rc;  // Go leaves the digest untouched on this path
-  d->stg.pending.clear();
-  d->base = d->shadow = s;
-  return EFES_OK;
-}
-
-int efes_sha1_get_state(efes_sha1* d, efes_sha1_state* out) {
-  if (!d || !out) return EFES_ERR_ARG;
-  const int rc = sha1_flush(d, false, nullptr);
-  if (rc) return rc;
-  *out = d->base;
-  return EFES_OK;
-}
-
-int efes_sha1_set_state(efes_sha1* d, const efes_sha1_state* in) {
-  if (!d || !in) return EFES_ERR_ARG;
-  d->stg.pending.clear();
-  d->base = d->shadow = *in;
-  return EFES_OK;
-}
-
-// ---- streaming CRC-32 ----------------------------------------------------------------------
-int efes_crc32_new(efes_ctx* ctx, efes_crc32** out) {
-  if (!ctx || !out) return EFES_ERR_ARG;
-  efes_crc32* d = new (std::nothrow) efes_crc32;
-  if (!d) return EFES_ERR_NOMEM;
-  d->stg.ctx = ctx;
-  d->st.crc = 0;
-  *out = d;
-  return EFES_OK;
-}
-
-void efes_crc32_free(efes_crc32* d) {
-  if (!d) return;
-  d->stg.release();
-  delete d;
-}
-
-void efes_crc32_reset(efes_crc32* d) {
-  if (!d) return;
-  d->stg.pending.clear();
-  d->st.crc = 0;
-}
-
-int efes_crc32_size(void) { return 4; }
-int efes_crc32_block_size(void) { return 1; }
-
-static int crc32_flush(efes_crc32* d) {
-  if (d->stg.latched) return d->stg.latched;
-  if (d->stg.pending.empty()) return EFES_OK;
-  return d->stg.run(nullptr, &d->st, false, nullptr);
-}
-
-int efes_crc32_write(efes_crc32* d, const void* p, size_t n) {
-  if (!d || (!p && n)) return EFES_ERR_ARG;
-  if (d->stg.latched) return d->stg.latched;
-  try {
-    d->stg.pending.insert(d->stg.pending.end(), static_cast<const uint8_t*>(p), static_cast<const uint8_t*>(p) + n);
-  } catch (...) {
-    return EFES_ERR_NOMEM;
-  }
-  if (d->stg.pending.size() >= kFlushBytes) return crc32_flush(d);
-  return EFES_OK;
-}
-
-int efes_crc32_sum32(efes_crc32* d, uint32_t* out) {
-  if (!d || !out) return EFES_ERR_ARG;
-  const int rc = crc32_flush(d);
-  if (rc) return rc;
-  *out = d->st.crc;
-  return EFES_OK;
-}
-
-int efes_crc32_sum(efes_crc32* d, uint8_t out[4]) {
-  uint32_t v;
-  const int rc = efes_crc32_sum32(d, &v);
-  if (rc) return rc;
-  put_be32(out, v);
-  return EFES_OK;
-}
-
-int efes_crc32_marshal_text(efes_crc32* d, char out[8]) {
-  if (!d || !out) return EFES_ERR_ARG;
-  const int rc = crc32_flush(d);
-  if (rc) return rc;
-  efes_crc32_state_marshal_text(&d->st, out);
-  return EFES_OK;
-}
-
-int efes_crc32_unmarshal_text(efes_crc32* d, const char* text, size_t n) {
-  if (!d) return EFES_ERR_ARG;
-  efes_crc32_state s;
-  const int rc = efes_crc32_state_unmarshal_text(&s, text, n);
-  if (rc) return rc;
-  d->stg.pending.clear();
-  d->st = s;
   return EFES_OK;
 }
 

@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <mutex>
+
 #include "../../include/efes_hash.h"
 
 namespace efes {
@@ -24,6 +26,12 @@ void build_tables(Tables* t);  // host
 // Go's sha1digest.Write bookkeeping of x/nx/len (sha1.go:58-79) without the compressions:
 // the host replays it so exported states carry Go's exact tail bytes (efes_api.cpp).
 int replay_write(efes_sha1_state* s, const uint8_t* p, size_t n);
+
+// The host-replayed Go state (x/nx/len; h as opened) of an upload (efes_queue.cpp).
+efes_sha1_state upload_shadow(const efes_upload* u);
+// The context's shared queue for the Go-surface digests, created on first use
+// (efes_stream.cpp); nullptr and *rc set on failure.
+efes_queue* stream_queue(efes_ctx* ctx, int* rc);
 
 // Launchers (host side, defined in efes_kernels.hip).
 hipError_t launch_deep(const efes_job* jobs, uint32_t njobs, const Tables* tabs, hipStream_t s);
@@ -54,4 +62,6 @@ struct efes_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   efes::Tables* d_tabs = nullptr;
+  std::mutex mu;                  // guards the lazy creation of `digests`
+  efes_queue* digests = nullptr;  // shared queue of the streaming digests (efes_stream.cpp)
 };

@@ -38,6 +38,7 @@ constexpr size_t kOffCrc = 104, kOffSum = 112, kOffStatus = 136, kOffJob = 144;
 
 struct efes_upload {
   efes_queue* q = nullptr;
+  uint32_t hashes = EFES_HASH_SHA1 | EFES_HASH_CRC32;
   uint32_t dslot = 0;            // device state slot
   int32_t cur = -1;              // staging chunk being filled (-1: none)
   uint64_t fill = 0;             // bytes in `cur`
@@ -145,8 +146,8 @@ void efes_queue::run() {
       efes_job& j = hj[i];
       j.data = z_slab + (size_t)p.slot * chunk;
       j.length = p.len;
-      j.sha1 = reinterpret_cast<efes_sha1_state*>(st);
-      j.crc32 = reinterpret_cast<efes_crc32_state*>(st + kOffCrc);
+      j.sha1 = (p.u->hashes & EFES_HASH_SHA1) ? reinterpret_cast<efes_sha1_state*>(st) : nullptr;
+      j.crc32 = (p.u->hashes & EFES_HASH_CRC32) ? reinterpret_cast<efes_crc32_state*>(st + kOffCrc) : nullptr;
       j.sum = nullptr;
       j.status = reinterpret_cast<int32_t*>(st + kOffStatus);
       j.flags = 0;
@@ -181,9 +182,9 @@ void efes_queue::run() {
 
 namespace {
 
-int enqueue_current(efes_upload* u, std::unique_lock<std::mutex>&) {  // q->mu held
+int enqueue_current(efes_upload* u, std::unique_lock<std::mutex>&, bool even_empty = false) {  // q->mu held
   efes_queue* q = u->q;
-  if (u->cur < 0 || u->fill == 0) return EFES_OK;
+  if (u->cur < 0 || (u->fill == 0 && !even_empty)) return EFES_OK;
   q->pending.push_back(Pending{u, (uint32_t)u->cur, u->fill});
   ++u->inflight;
   u->cur = -1;
@@ -263,12 +264,14 @@ void efes_queue_destroy(efes_queue* q) {
   delete q;
 }
 
-int efes_upload_open(efes_queue* q, const efes_sha1_state* sha1, const efes_crc32_state* crc, efes_upload** out) {
-  if (!q || !out) return EFES_ERR_ARG;
+int efes_upload_open(efes_queue* q, uint32_t hashes, const efes_sha1_state* sha1, const efes_crc32_state* crc,
+                     efes_upload** out) {
+  if (!q || !out || !hashes || (hashes & ~(EFES_HASH_SHA1 | EFES_HASH_CRC32))) return EFES_ERR_ARG;
   *out = nullptr;
   efes_upload* u = new (std::nothrow) efes_upload;
   if (!u) return EFES_ERR_NOMEM;
   u->q = q;
+  u->hashes = hashes;
   {
     std::lock_guard<std::mutex> lk(q->mu);
     if (q->free_states.empty()) {
@@ -303,9 +306,23 @@ int efes_upload_open(efes_queue* q, const efes_sha1_state* sha1, const efes_crc3
 int efes_upload_write(efes_upload* u, const void* p, size_t n) {
   if (!u || (!p && n)) return EFES_ERR_ARG;
   if (u->latched) return u->latched;
+  const bool full_tail = u->shadow.nx == 64;
   const int rc = efes::replay_write(&u->shadow, static_cast<const uint8_t*>(p), n);
   if (rc) return u->latched = rc;  // the Go Write would panic (nx > 64)
   efes_queue* q = u->q;
+  if (n == 0 && full_tail && (u->hashes & EFES_HASH_SHA1)) {
+    // Go compresses a full pending tail even on an empty Write (sha1.go:61-69); run a
+    // zero-length job so the device state follows.
+    std::unique_lock<std::mutex> lk(q->mu);
+    enqueue_current(u, lk);
+    q->freed.wait(lk, [&] { return !q->free_chunks.empty() || q->fault; });
+    if (q->fault) return u->latched = q->fault;
+    u->cur = (int32_t)q->free_chunks.back();
+    q->free_chunks.pop_back();
+    u->fill = 0;
+    enqueue_current(u, lk, true);
+    return EFES_OK;
+  }
   const uint8_t* src = static_cast<const uint8_t*>(p);
   // `cur`/`fill` belong to the thread that owns this upload, so filling the current chunk
   // takes no lock; the queue lock is taken only to get a chunk and to hand a full one over.
@@ -369,8 +386,8 @@ int efes_upload_sum(efes_upload* u, uint8_t out[24]) {
   efes_job job{};
   job.data = nullptr;
   job.length = 0;
-  job.sha1 = reinterpret_cast<efes_sha1_state*>(st);
-  job.crc32 = reinterpret_cast<efes_crc32_state*>(st + kOffCrc);
+  job.sha1 = (u->hashes & EFES_HASH_SHA1) ? reinterpret_cast<efes_sha1_state*>(st) : nullptr;
+  job.crc32 = (u->hashes & EFES_HASH_CRC32) ? reinterpret_cast<efes_crc32_state*>(st + kOffCrc) : nullptr;
   job.sum = st + kOffSum;
   job.status = reinterpret_cast<int32_t*>(st + kOffStatus);
   job.flags = EFES_JOB_FINALIZE;
@@ -389,6 +406,14 @@ int efes_upload_sum(efes_upload* u, uint8_t out[24]) {
   memcpy(out, back, 24);
   return EFES_OK;
 }
+
+}  // extern "C"
+
+namespace efes {
+efes_sha1_state upload_shadow(const efes_upload* u) { return u->shadow; }
+}  // namespace efes
+
+extern "C" {
 
 void efes_upload_close(efes_upload* u) {
   if (!u) return;

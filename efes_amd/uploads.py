@@ -25,8 +25,8 @@ class UploadQueue:
               "efes_queue_create")
         self.handle = h
 
-    def open(self, state: Sha1State | None = None, crc: int | None = None) -> "Upload":
-        return Upload(self, state, crc)
+    def open(self, state: Sha1State | None = None, crc: int | None = None, hashes: int = 3) -> "Upload":
+        return Upload(self, state, crc, hashes)
 
     def close(self) -> None:
         if self.handle:
@@ -49,12 +49,12 @@ class UploadQueue:
 class Upload:
     """One upload's (SHA-1, CRC-32) pair, fed in the MultiWriter order of filereceiver.go:208."""
 
-    def __init__(self, queue: UploadQueue, state: Sha1State | None = None, crc: int | None = None):
+    def __init__(self, queue: UploadQueue, state: Sha1State | None = None, crc: int | None = None, hashes: int = 3):
         self.queue = queue
         h = ctypes.c_void_p()
         st = ctypes.byref(state) if state is not None else None
         cs = ctypes.byref(Crc32State(crc & 0xFFFFFFFF)) if crc is not None else None
-        check(lib().efes_upload_open(queue.handle, st, cs, ctypes.byref(h)), "efes_upload_open")
+        check(lib().efes_upload_open(queue.handle, hashes, st, cs, ctypes.byref(h)), "efes_upload_open")
         self._h = h
 
     def write(self, p) -> int:

@@ -157,18 +157,29 @@ int efes_host_free(efes_ctx* ctx, void* p);
  * and must be < max_chunks (each open upload may hold one partly filled chunk). */
 typedef struct efes_queue efes_queue;
 typedef struct efes_upload efes_upload;
+#define EFES_HASH_SHA1 0x1u  /* which digests an upload keeps (a MultiWriter of both is 0x3) */
+#define EFES_HASH_CRC32 0x2u
 int efes_queue_create(efes_ctx* ctx, uint64_t chunk_bytes, uint32_t max_chunks, uint32_t max_uploads,
                       efes_queue** out);
 void efes_queue_destroy(efes_queue* q); /* finishes launched work; close uploads first */
-/* sha1 / crc32: initial states (host), NULL = NewSha1() / NewCRC32IEEE() */
-int efes_upload_open(efes_queue* q, const efes_sha1_state* sha1, const efes_crc32_state* crc32, efes_upload** out);
+/* hashes: EFES_HASH_SHA1 | EFES_HASH_CRC32; sha1 / crc32: initial states (host), NULL =
+ * NewSha1() / NewCRC32IEEE().  Sums of a digest the upload does not keep read as zeros. */
+int efes_upload_open(efes_queue* q, uint32_t hashes, const efes_sha1_state* sha1, const efes_crc32_state* crc32,
+                     efes_upload** out);
 int efes_upload_write(efes_upload* u, const void* p, size_t n);
 int efes_upload_flush(efes_upload* u);
 int efes_upload_state(efes_upload* u, efes_sha1_state* sha1, efes_crc32_state* crc32);
 int efes_upload_sum(efes_upload* u, uint8_t out[24]);
 void efes_upload_close(efes_upload* u); /* drops bytes staged since the last sync point */
 
-/* ---- layer 2: streaming digests mirroring the Go surface ---------------------------- */
+/* ---- layer 2: streaming digests mirroring the Go surface ----------------------------
+ * Each object is an upload (above) of the context's shared digest queue that keeps only its
+ * own hash, so unchanged Go code -- MultiWriter(f, CRC32, Sha1) in every request goroutine --
+ * is batched across all concurrent requests: Write stages into pinned memory and returns,
+ * Sum / Sum32 / MarshalText are the sync points.  The shared queue holds
+ * EFES_DIGEST_STAGING_MIB (env, default 256) of pinned staging in 64 KiB chunks; a Write
+ * blocks while all chunks are in flight, and EFES_ERR_NOMEM is returned when more digests
+ * are being written at once than the pool has chunks. */
 typedef struct efes_sha1 efes_sha1;
 typedef struct efes_crc32 efes_crc32;
 

@@ -641,3 +641,56 @@ def test_bench_emits_driver_json(env):
     assert d["steps"] == 2 and d["n_gpus"] == 1 and d["value"] > 0
     assert d["roofline"]["bound"] == "hbm" and 0 < d["roofline"]["frac"] < 1
     assert d["cpu_baseline"]["digests_match_gpu"] and d["host_inclusive"]["digests_match_device_path"]
+
+
+def test_streaming_digests_batch_across_threads(env, oracle):
+    """Unchanged Go-surface digests (MultiWriter(CRC32, Sha1) per request) from 12 threads:
+    they share the context's digest queue, so their Writes batch into common launches."""
+    import threading
+    h = env["hashing"]
+    rng = random.Random(3)
+    jobs = []
+    for i in range(36):
+        n = rng.choice([0, 5, 64, 1000, 65536, 300001, rng.randint(0, 2 << 20)])
+        jobs.append(oracle.fill_synthetic(n, 500 + i).tobytes())
+    res = [None] * len(jobs)
+    errs = []
+
+    def worker(t):
+        try:
+            for i in range(t, len(jobs), 12):
+                sha, crc = h.new_sha1(), h.new_crc32_ieee()
+                data = jobs[i]
+                for a in range(0, len(data), 32 * 1024):  # io.Copy buffers through the MultiWriter
+                    crc.write(data[a:a + 32 * 1024])
+                    sha.write(data[a:a + 32 * 1024])
+                res[i] = (sha.sum().hex(), crc.sum32(), sha.marshal_text().decode())
+        except Exception as e:  # pragma: no cover
+            errs.append(repr(e))
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(12)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert not errs, errs
+    for data, (sha, crc, mt) in zip(jobs, res):
+        assert sha == hashlib.sha1(data).hexdigest() and crc == zlib.crc32(data)
+        o = oracle.Sha1()
+        for a in range(0, len(data), 32 * 1024):
+            o.write(data[a:a + 32 * 1024])
+        assert mt == o.marshal_text()
+
+
+def test_streaming_full_tail_empty_write(env, oracle):
+    """nx == 64 then an empty Write: Go compresses the pending block (sha1.go:61-69)."""
+    h = env["hashing"]
+    o = oracle.Sha1()
+    o.st.x[:] = bytes(range(64))
+    o.st.nx, o.st.len = 64, 64
+    text = o.marshal_text()
+    d = h.new_sha1()
+    d.unmarshal_text(text.encode())
+    d.write(b"")
+    o.write(b"")
+    assert d.marshal_text().decode() == o.marshal_text()
+    assert d.sum().hex() == o.hexdigest()

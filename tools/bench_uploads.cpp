@@ -61,7 +61,7 @@ int main(int argc, char** argv) {
         const size_t n = std::min(mine.size() - g, (size_t)K);
         std::vector<efes_upload*> ups(n, nullptr);
         for (auto& up : ups)
-          if (efes_upload_open(q, nullptr, nullptr, &up)) { ++errs; return; }
+          if (efes_upload_open(q, EFES_HASH_SHA1 | EFES_HASH_CRC32, nullptr, nullptr, &up)) { ++errs; return; }
         for (size_t a = 0; a < S; a += W)
           for (auto* up : ups)
             if (efes_upload_write(up, src.data() + a, a + W <= S ? W : S - a)) { ++errs; return; }

@@ -93,13 +93,76 @@ extern "C" {
 int efes_host_alloc(efes_ctx* ctx, size_t bytes, void** out) {
   if (!ctx || !out) return EFES_ERR_ARG;
   DeviceGuard g(ctx->device);
-  return hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault) == hipSuccess ? EFES_OK : EFES_ERR_HIP;
+  return hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocMapped) == hipSuccess ? EFES_OK : EFES_ERR_HIP;
 }
 
 int efes_host_free(efes_ctx* ctx, void* p) {
   if (!ctx) return EFES_ERR_ARG;
   DeviceGuard g(ctx->device);
   return hipHostFree(p) == hipSuccess ? EFES_OK : EFES_ERR_HIP;
+}
+
+// EFES_HOST_ZERO_COPY: the data is pinned, device-mapped host memory (efes_host_alloc); one DEEP
+// launch reads it in place over PCIe (coalesced 4 KiB per wave, prefetched a super-step ahead
+// of the chain) -- no staging, no segments.
+static int hash_host_mapped(efes_ctx* ctx, const efes_job* jobs, uint32_t n, efes_host_stats* stats) {
+  std::vector<efes_job> hj(jobs, jobs + n);
+  uint64_t total = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    total += jobs[i].length;
+    if (!jobs[i].length) continue;
+    hipPointerAttribute_t attr;
+    if (hipPointerGetAttributes(&attr, jobs[i].data) != hipSuccess || !attr.devicePointer) return EFES_ERR_ARG;
+    hj[i].data = attr.devicePointer;  // device address of this exact host byte
+  }
+  HipBuf d_states, d_crcs, d_sums, d_status, d_jobs;
+  hipError_t e = d_states.alloc(sizeof(efes_sha1_state) * n);
+  if (e == hipSuccess) e = d_crcs.alloc(sizeof(efes_crc32_state) * n);
+  if (e == hipSuccess) e = d_sums.alloc(24ull * n);
+  if (e == hipSuccess) e = d_status.alloc(sizeof(int32_t) * n);
+  if (e == hipSuccess) e = d_jobs.alloc(sizeof(efes_job) * n);
+  if (e != hipSuccess) return EFES_ERR_HIP;
+  std::vector<efes_sha1_state> hs(n);
+  std::vector<efes_crc32_state> hc(n);
+  std::vector<uint8_t> hsum(24ull * n);
+  std::vector<int32_t> hst(n, EFES_OK);
+  for (uint32_t i = 0; i < n; ++i) {
+    if (jobs[i].sha1) hs[i] = *jobs[i].sha1;
+    else memset(&hs[i], 0, sizeof hs[i]);
+    hc[i].crc = jobs[i].crc32 ? jobs[i].crc32->crc : 0u;
+    hj[i].sha1 = jobs[i].sha1 ? d_states.as<efes_sha1_state>() + i : nullptr;
+    hj[i].crc32 = jobs[i].crc32 ? d_crcs.as<efes_crc32_state>() + i : nullptr;
+    hj[i].sum = (jobs[i].flags & EFES_JOB_FINALIZE) ? d_sums.as<uint8_t>() + 24ull * i : nullptr;
+    hj[i].status = d_status.as<int32_t>() + i;
+  }
+  hipStream_t s = ctx->stream;
+  e = hipMemcpyAsync(d_states.p, hs.data(), sizeof(efes_sha1_state) * n, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(d_crcs.p, hc.data(), sizeof(efes_crc32_state) * n, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(d_status.p, hst.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(d_jobs.p, hj.data(), sizeof(efes_job) * n, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return EFES_ERR_HIP;
+  const auto t0 = std::chrono::steady_clock::now();
+  int rc = efes_hash_submit_mode(ctx, d_jobs.as<efes_job>(), n, s, EFES_MODE_DEEP);
+  if (rc) return rc;
+  e = hipMemcpyAsync(hs.data(), d_states.p, sizeof(efes_sha1_state) * n, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(hc.data(), d_crcs.p, sizeof(efes_crc32_state) * n, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(hsum.data(), d_sums.p, 24ull * n, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(hst.data(), d_status.p, sizeof(int32_t) * n, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return EFES_ERR_DEVICE_FAULT;
+  for (uint32_t i = 0; i < n; ++i) {
+    if (jobs[i].sha1) *jobs[i].sha1 = hs[i];
+    if (jobs[i].crc32) *jobs[i].crc32 = hc[i];
+    if (jobs[i].sum && (jobs[i].flags & EFES_JOB_FINALIZE)) memcpy(jobs[i].sum, hsum.data() + 24ull * i, 24);
+    if (jobs[i].status) *jobs[i].status = hst[i];
+  }
+  if (stats) {
+    stats->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    stats->bytes = total;
+    stats->segments = 1;
+  }
+  return EFES_OK;
 }
 
 int efes_hash_host(efes_ctx* ctx, const efes_job* jobs, uint32_t n, uint64_t segment_bytes, efes_host_stats* stats) {
@@ -110,6 +173,10 @@ int efes_hash_host(efes_ctx* ctx, const efes_job* jobs, uint32_t n, uint64_t seg
     if ((jobs[i].flags & ~(EFES_JOB_FINALIZE | EFES_JOB_INIT)) || (!jobs[i].data && jobs[i].length) ||
         ((jobs[i].flags & EFES_JOB_FINALIZE) && !jobs[i].sum))
       return EFES_ERR_ARG;
+  if (segment_bytes == EFES_HOST_ZERO_COPY) {
+    DeviceGuard g(ctx->device);
+    return hash_host_mapped(ctx, jobs, n, stats);
+  }
   const uint64_t seg = segment_bytes ? (segment_bytes + 63) & ~uint64_t(63) : (uint64_t)1 << 20;
   uint64_t nseg = 1;
   for (uint32_t i = 0; i < n; ++i) nseg = std::max<uint64_t>(nseg, (jobs[i].length + seg - 1) / seg);

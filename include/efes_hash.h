@@ -131,6 +131,11 @@ int efes_fill_synthetic(efes_ctx* ctx, void* dst_device, size_t bytes, uint64_t 
  * segment-sized Writes, sha1.go:75-77).  Messages whose host addresses advance by a constant stride are copied with one
  * 2D copy per segment.  For the full PCIe rate the data should be pinned (efes_host_alloc).
  * Synchronous; stats (may be NULL) time the pipeline from the first copy to the last result. */
+/* segment_bytes == EFES_HOST_ZERO_COPY: every data pointer is pinned, device-mapped host memory
+ * (efes_host_alloc) and one launch reads it in place over PCIe: no staging copies, no segments
+ * (EFES_ERR_ARG if a pointer is not device-accessible).  Stats time the launch and the result
+ * copies. */
+#define EFES_HOST_ZERO_COPY ((uint64_t)-1)
 typedef struct efes_host_stats {
     double seconds;    /* wall time of the copy+hash pipeline */
     uint64_t bytes;    /* message bytes moved and hashed */
@@ -140,7 +145,7 @@ typedef struct efes_host_stats {
 
 int efes_hash_host(efes_ctx* ctx, const efes_job* jobs_host, uint32_t njobs, uint64_t segment_bytes,
                    efes_host_stats* stats);
-int efes_host_alloc(efes_ctx* ctx, size_t bytes, void** out); /* pinned host memory (hipHostMalloc) */
+int efes_host_alloc(efes_ctx* ctx, size_t bytes, void** out); /* pinned, device-mapped host memory */
 int efes_host_free(efes_ctx* ctx, void* p);
 
 /* ---- concurrent uploads: batching dispatcher ------------------------------------------

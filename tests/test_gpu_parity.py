@@ -694,3 +694,38 @@ def test_streaming_full_tail_empty_write(env, oracle):
     o.write(b"")
     assert d.marshal_text().decode() == o.marshal_text()
     assert d.sum().hex() == o.hexdigest()
+
+
+def test_host_ingest_zero_copy(env, oracle):
+    """EFES_HOST_ZERO_COPY: the kernel reads pinned host chunks in place; pageable data is refused."""
+    from efes_amd._lib import EFES_HOST_ZERO_COPY
+    from efes_amd.batch import HostBatch, PinnedHostBuffer
+    rng = random.Random(12)
+    lengths = [0, 1, 64, 65, 4095, 100000] + [rng.randint(0, 300000) for _ in range(40)]
+    offsets, pos = [], 0
+    for L in lengths:
+        offsets.append(pos)
+        pos += L + rng.randint(0, 7)
+    buf = PinnedHostBuffer(pos + 8, env["ctx"])
+    try:
+        buf.array[:] = oracle.fill_synthetic(pos + 8, 6)
+        rngs = random.Random(2)
+        states, crcs = midstream_states(oracle, env, len(lengths), rngs)
+        hb = HostBatch(buf.ptr, offsets, lengths, fresh=False, states=states, crcs=crcs, ctx=env["ctx"])
+        st = hb.run(EFES_HOST_ZERO_COPY)
+        assert st.segments == 1 and st.bytes == sum(lengths)
+        for i, (o, L) in enumerate(zip(offsets, lengths)):
+            d = buf.array[o:o + L].tobytes()
+            e_status, e_state, e_crc, e_sum = oracle_expect(oracle, states[i], d, int(crcs[i]))
+            assert hb.status[i] == e_status
+            assert list(hb.states[i]["h"]) == e_state["h"] and bytes(hb.states[i]["x"]) == e_state["x"]
+            assert int(hb.crcs[i]) == e_crc
+            if e_sum is not None:
+                assert bytes(hb.sums[i][:20]) == e_sum
+    finally:
+        buf.free()
+    pageable = oracle.fill_synthetic(4096, 1)
+    hb = HostBatch(pageable.ctypes.data, [0], [4096], ctx=env["ctx"])
+    with pytest.raises(env["efes"].EfesError) as e:
+        hb.run(EFES_HOST_ZERO_COPY)
+    assert e.value.code == env["efes"].EFES_ERR_ARG

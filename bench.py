@@ -97,6 +97,32 @@ def load_traffic(kernel: str, workload_key: str):
     return None if best is None else float(best["bytes_per_launch"])
 
 
+def config0_cpu(data, chunk: int):
+    """BASELINE configs[0]: sha1file.go over one 4 MiB chunk on the CPU path (the oracle's
+    Sha1File, 32 KiB reads as io.Copy issues them, one seek-back-and-reread like a retried
+    PATCH, sha1file.go:23-49), single thread; the digest is checked against the GPU's."""
+    import hashlib
+
+    from oracle import oracle
+
+    host = data[:chunk].cpu().numpy().tobytes()
+    best = None
+    for _ in range(3):
+        f = oracle.Sha1File(host)  # wraps the chunk (the ReadSeeker), outside the timed region
+        t0 = time.perf_counter()
+        for a in range(0, chunk // 2, 32 << 10):
+            f.read(32 << 10)
+        f.seek(chunk // 4)  # retry: seek back, bytes up to `calculated` are not hashed again
+        while f.read(32 << 10):
+            pass
+        dt = time.perf_counter() - t0
+        best = dt if best is None else min(best, dt)
+        digest = f.sum()
+    return {"value": round(chunk / best / (1 << 20), 1), "unit": "MiB/s", "cores": 1, "kind": "port",
+            "sample": f"Sha1File over one {chunk >> 20} MiB chunk, 32 KiB reads, one seek-back, best of 3",
+            "digest_matches": digest == hashlib.sha1(host).digest()}
+
+
 def cpu_baseline(batch, data, n_chunks: int, chunk: int, threads: int, do_crc: bool, min_seconds: float = 10.0):
     """The oracle (C restatement of sha1.go block + crc32.go slicingUpdate) over the same chunks."""
     import numpy as np
@@ -393,6 +419,7 @@ def main(argv=None):
             threads = args.cpu_threads or host_threads()
             out["cpu_baseline"] = cpu_baseline(batches[0], data, min(n, args.cpu_max_chunks), chunk, threads,
                                                not args.sha1_only, args.cpu_seconds)
+            out["config0_cpu"] = config0_cpu(data, chunk)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:

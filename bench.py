@@ -272,6 +272,31 @@ def make_workload(args, rank: int, world: int, ctx, device: str, stream):
                                    "launches": len(batches)}
 
 
+# Instruction-issue ceilings: a wave64 integer VALU instruction holds its SIMD
+# for 4 cycles (SQ_INSTS_VALU == SQ_ACTIVE_INST_VALU quad-cycles in profiles/r01_pmc), and
+#   DEEP: one message per wave; its SHA-1 chain is 405 VALU per 64-B block (80 rounds x 5 + 5);
+#   WIDE: one message per lane; 740 VALU per 64-B block per wave (592 SHA-1 rounds+schedule,
+#         16 byte swaps, ~130 CRC-32 slicing-by-8 address/xor ops; 615 with SHA-1 only).
+CLOCK_HZ = 2.4e9
+N_SIMD = 1024
+VALU_CYC = 4
+
+
+def binding_roofline(kernel: str, achieved_gbs: float, concurrent_msgs: int, sha1_only: bool):
+    if kernel == "deep_kernel":
+        ceiling = min(concurrent_msgs, N_SIMD) * 64 * CLOCK_HZ / (405 * VALU_CYC) / 1e9
+        model = ("serial SHA-1 chain: each of min(messages, 1024 SIMDs) messages advances one 64-B block per "
+                 "405 VALU x 4 cycles at 2.4 GHz (one wave per message)")
+    else:
+        per_block = 615 if sha1_only else 740
+        lanes = min(concurrent_msgs, N_SIMD * 64 * 8)
+        ceiling = min(lanes / 64, N_SIMD) * 64 * 64 * CLOCK_HZ / (per_block * VALU_CYC) / 1e9
+        model = (f"VALU issue: {per_block} VALU per 64-B block per wave of 64 messages, 4 cycles each, "
+                 "every SIMD busy at 2.4 GHz")
+    return {"bound": "valu-issue", "achieved": round(achieved_gbs, 2), "ceiling": round(ceiling, 2), "unit": "GB/s",
+            "frac": round(achieved_gbs / ceiling, 4), "model": model}
+
+
 def run_timed(batches, steps: int, warmup: int, mode: int, device: str, stream, dist, progress: bool = False):
     """W untimed warm-up launches, then exactly `steps` launches bracketed by barrier +
     synchronize; returns (wall seconds of this rank, average kernel ms from HIP events recorded
@@ -326,6 +351,7 @@ def ingest_leg(args, rank: int, world: int, ctx, device: str, stream, mode: int)
             "chunks": config["chunks_per_gpu"], "launches": config["launches"], "kernel": "wide_kernel",
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 5), "kernel_ms": round(kernel_ms, 3)},
+            "binding_roofline": binding_roofline("wide_kernel", achieved, batches[0].n, args.sha1_only),
             "note": "many concurrent chunks per GPU (configs[4] per-GPU queue); not `value`"}
 
 
@@ -406,6 +432,7 @@ def main(argv=None):
             "kernel_ms": round(kernel_ms, 4),
             "algorithmic_bytes_per_launch": int(per_launch),
         },
+        "binding_roofline": binding_roofline(kernel_name, achieved, njobs, args.sha1_only),
         "cpu_baseline": None,
     }
     if args.workload == "chunks4m":

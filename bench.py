@@ -345,13 +345,14 @@ def ingest_leg(args, rank: int, world: int, ctx, device: str, stream, mode: int)
     total = sum(step_bytes)
     per_launch = total / len(batches)
     achieved = per_launch / (kernel_ms * 1e-3) / 1e9
+    per_launch_jobs = batches[0].n
     del data, batches
     torch.cuda.empty_cache()
     return {"value": round(total / wall / GiB, 3), "unit": "GiB/s", "workload": config["workload"],
             "chunks": config["chunks_per_gpu"], "launches": config["launches"], "kernel": "wide_kernel",
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 5), "kernel_ms": round(kernel_ms, 3)},
-            "binding_roofline": binding_roofline("wide_kernel", achieved, batches[0].n, args.sha1_only),
+            "binding_roofline": binding_roofline("wide_kernel", achieved, per_launch_jobs, args.sha1_only),
             "note": "many concurrent chunks per GPU (configs[4] per-GPU queue); not `value`"}
 
 

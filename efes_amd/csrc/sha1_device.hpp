@@ -74,6 +74,19 @@ struct ChainQuad<20> {
   __device__ __forceinline__ static void run(uint32_t (&)[5], const uint4* __restrict__) {}
 };
 
+// ---- chain from W[i]+K[i] held in this lane's own registers (80 VGPRs).
+template <int R>
+struct ChainRegs {
+  __device__ __forceinline__ static void run(uint32_t (&s)[5], const uint32_t (&wk)[80]) {
+    round_wk<R>(s, wk[R]);
+    ChainRegs<R + 1>::run(s, wk);
+  }
+};
+template <>
+struct ChainRegs<80> {
+  __device__ __forceinline__ static void run(uint32_t (&)[5], const uint32_t (&)[80]) {}
+};
+
 // h += compress(WK) -- sha1.go:141-197 with the schedule already expanded.
 __device__ __forceinline__ void compress_wk(uint32_t (&h)[5], const uint4* __restrict__ wk4) {
   uint32_t s[5] = {h[0], h[1], h[2], h[3], h[4]};

@@ -43,7 +43,8 @@ def parse_args(argv=None):
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--chunks", type=int, default=1024, help="chunks per GPU")
     p.add_argument("--chunk-bytes", type=int, default=4 << 20)
-    p.add_argument("--mode", choices=["auto", "deep", "wide"], default="auto")
+    p.add_argument("--mode", choices=["auto", "deep", "wide", "plan", "group4", "group8", "group16", "group32"],
+                   default="auto", help="auto: AUTO for chunks4m/ingest, plan (efes_plan_batch) for mixed")
     p.add_argument("--workload", choices=["chunks4m", "mixed", "ingest", "uploads"], default="chunks4m",
                    help="chunks4m = BASELINE configs[1]/[2] (the metric); mixed = configs[3]; ingest = configs[4]")
     p.add_argument("--pool-gib", type=int, default=64, help="device pool aliased by mixed/ingest chunks")
@@ -361,7 +362,8 @@ def main(argv=None):
     import torch
 
     from efes_amd import MODE_AUTO, MODE_DEEP, MODE_WIDE
-    from efes_amd._lib import kAutoDeepMaxJobs
+    from efes_amd._lib import MODE_GROUP, lib
+    from efes_amd.batch import MODE_PLAN
     from efes_amd.hashing import default_context
     from efes_amd.shard import env_rank, max_over_ranks
 
@@ -382,7 +384,9 @@ def main(argv=None):
     torch.cuda.set_device(dev_index)
     ctx = default_context(dev_index)
     stream = torch.cuda.Stream(device=device)
-    mode = {"auto": MODE_AUTO, "deep": MODE_DEEP, "wide": MODE_WIDE}[args.mode]
+    modes = {"auto": MODE_AUTO, "deep": MODE_DEEP, "wide": MODE_WIDE, "plan": MODE_PLAN}
+    modes.update({f"group{g}": v for g, v in MODE_GROUP.items()})
+    mode = modes["plan" if args.mode == "auto" and args.workload == "mixed" else args.mode]
 
     if args.workload == "uploads":
         res = uploads_workload(args, ctx)
@@ -394,6 +398,9 @@ def main(argv=None):
         return
     with torch.cuda.stream(stream):
         data, batches, step_bytes, config = make_workload(args, rank, world, ctx, device, stream)
+        if mode == MODE_PLAN:
+            for b in batches:
+                b.make_plan()  # host-side planning stays outside the timed region
         steps = args.steps if len(batches) == 1 else len(batches)
         wall, kernel_ms = run_timed(batches, steps, args.warmup, mode, device, stream, dist, args.progress)
     wall = max_over_ranks(wall, device if args.dist_backend == "nccl" else None)  # slowest rank
@@ -401,8 +408,18 @@ def main(argv=None):
     bytes_timed = sum(step_bytes[k % len(step_bytes)] for k in range(steps))
     value = world * bytes_timed / wall / GiB
     njobs = batches[0].n
-    deep = mode == MODE_DEEP or (mode == MODE_AUTO and njobs <= kAutoDeepMaxJobs)
-    kernel_name = "deep_kernel" if deep else "wide_kernel"
+    launched = lib().efes_auto_mode(ctx.handle, njobs) if mode == MODE_AUTO else mode
+    kernel_name = {MODE_DEEP: "deep_kernel", MODE_WIDE: "wide_kernel"}.get(launched, "group_kernel")
+    if launched in MODE_GROUP.values():
+        kernel_name = f"group_kernel<{ {v: g for g, v in MODE_GROUP.items()}[launched] }>"
+    plan = None
+    if mode == MODE_PLAN:
+        p0 = batches[0].plan
+        names = {MODE_DEEP: "deep_kernel", MODE_WIDE: "wide_kernel"}
+        names.update({v: f"group_kernel<{g}>" for g, v in MODE_GROUP.items()})
+        plan = {"parts": [{"jobs": j, "kernel": names[m], "exclusive_cus": x} for j, m, x in p0.parts()],
+                "model_seconds": round(p0.est_seconds, 4)}
+        kernel_name = " + ".join(p["kernel"] for p in plan["parts"]) + " (concurrent streams)"
     per_launch = bytes_timed / steps
     workload_key = f"{config['workload']}:{'sha1' if args.sha1_only else 'sha1+crc32'}"
     if args.workload == "chunks4m":
@@ -433,9 +450,12 @@ def main(argv=None):
             "kernel_ms": round(kernel_ms, 4),
             "algorithmic_bytes_per_launch": int(per_launch),
         },
-        "binding_roofline": binding_roofline(kernel_name, achieved, njobs, args.sha1_only),
+        "binding_roofline": (binding_roofline(kernel_name, achieved, njobs, args.sha1_only)
+                             if kernel_name in ("deep_kernel", "wide_kernel") else None),
         "cpu_baseline": None,
     }
+    if plan:
+        out["config"]["plan"] = plan
     if args.workload == "chunks4m":
         n, chunk = args.chunks, args.chunk_bytes
         if args.host_inclusive == "on" or (args.host_inclusive == "auto" and world == 1):

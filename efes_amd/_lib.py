@@ -31,12 +31,30 @@ EFES_JOB_INIT = 0x2
 EFES_HASH_SHA1, EFES_HASH_CRC32 = 0x1, 0x2
 EFES_HOST_ZERO_COPY = (1 << 64) - 1
 MODE_AUTO, MODE_DEEP, MODE_WIDE = 0, 1, 2
-kAutoDeepMaxJobs = 1536  # efes_internal.hpp: AUTO picks DEEP up to this many jobs
+MODE_GROUP = {4: 3, 8: 4, 16: 5, 32: 6}  # grouped DEEP: lanes per job -> EFES_MODE_GROUPn
 
 
 class HostStats(ctypes.Structure):
     _fields_ = [("seconds", ctypes.c_double), ("bytes", ctypes.c_uint64), ("segments", ctypes.c_uint32),
                 ("_reserved", ctypes.c_uint32)]
+
+
+class PlanPart(ctypes.Structure):
+    _fields_ = [("jobs", ctypes.c_uint32), ("mode", ctypes.c_int32), ("exclusive", ctypes.c_uint32),
+                ("_reserved", ctypes.c_uint32)]
+
+
+PLAN_MAX_PARTS = 3
+
+
+class Plan(ctypes.Structure):
+    """efes_plan: consecutive parts of a longest-first batch, each in its own kernel shape."""
+    _fields_ = [("njobs", ctypes.c_uint32), ("nparts", ctypes.c_uint32), ("part", PlanPart * PLAN_MAX_PARTS),
+                ("est_seconds", ctypes.c_double)]
+
+    def parts(self) -> list[tuple[int, int, bool]]:
+        """[(jobs, mode, exclusive)] of the parts in use."""
+        return [(int(p.jobs), int(p.mode), bool(p.exclusive)) for p in self.part[: self.nparts]]
 
 
 class Sha1State(ctypes.Structure):
@@ -76,6 +94,9 @@ SIGNATURES = {
     "efes_ctx_stream": (_VP, [_VP]),
     "efes_hash_submit": (_I, [_VP, _VP, _U32, _VP]),
     "efes_hash_submit_mode": (_I, [_VP, _VP, _U32, _VP, _I]),
+    "efes_auto_mode": (_I, [_VP, _U32]),
+    "efes_plan_batch": (_I, [_VP, _P(_U64), _U32, _P(_U32), _P(Plan)]),
+    "efes_hash_submit_plan": (_I, [_VP, _VP, _P(Plan), _VP]),
     "efes_sync": (_I, [_VP, _VP]),
     "efes_device_alloc": (_I, [_VP, _S, _P(_VP)]),
     "efes_device_free": (_I, [_VP, _VP]),

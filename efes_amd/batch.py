@@ -12,6 +12,8 @@ import numpy as np
 from ._lib import EFES_JOB_FINALIZE, EFES_JOB_INIT, JOB_DTYPE, MODE_AUTO, SHA1_STATE_DTYPE
 from .hashing import Context, default_context
 
+MODE_PLAN = -1  # run(): efes_plan_batch + efes_hash_submit_plan instead of one fixed kernel shape
+
 IV = np.array([0x67452301, 0xEFCDAB89, 0x98BADCFE, 0x10325476, 0xC3D2E1F0], dtype=np.uint32)
 
 
@@ -77,11 +79,27 @@ class DeviceBatch:
 
     def submit(self, mode: int = MODE_AUTO) -> None:
         """Enqueue all jobs on torch's current stream (ordered after the data it wrote)."""
-        self.ctx.submit(self.jobs.data_ptr(), self.n, self.stream(), mode)
+        if mode == MODE_PLAN:
+            self.submit_planned()
+        else:
+            self.ctx.submit(self.jobs.data_ptr(), self.n, self.stream(), mode)
 
     def run(self, mode: int = MODE_AUTO) -> None:
         self.submit(mode)
         self.torch.cuda.synchronize(self.device)
+
+    def make_plan(self) -> None:
+        """efes_plan_batch over the job lengths; keeps a longest-first copy of the job array."""
+        order, self.plan = self.ctx.plan(self.jobs_host["length"])
+        self.jobs_planned = self.torch.from_numpy(self.jobs_host[order].view(np.uint8).copy()).to(self.device)
+        self.torch.cuda.synchronize(self.device)
+
+    def submit_planned(self) -> None:
+        """The planned launch (DEEP/grouped part concurrent with the WIDE part) on torch's current stream."""
+        if not hasattr(self, "plan"):
+            self.make_plan()
+        self.ctx.submit_plan(self.jobs_planned.data_ptr(), self.plan, self.stream())
+
 
     # ---- results (host copies)
     def status_host(self) -> np.ndarray:

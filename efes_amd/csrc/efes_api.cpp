@@ -168,7 +168,13 @@ int efes_ctx_create(int device, efes_ctx** out) {
   Tables* host = static_cast<Tables*>(malloc(sizeof(Tables)));
   if (!host) { delete ctx; return EFES_ERR_NOMEM; }
   efes::build_tables(host);
+  ctx->cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
   hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming);
+  for (int i = 0; i < EFES_PLAN_MAX_PARTS - 1 && e == hipSuccess; ++i) {
+    e = hipStreamCreateWithFlags(&ctx->side[i], hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_join[i], hipEventDisableTiming);
+  }
   if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&ctx->d_tabs), sizeof(Tables));
   if (e == hipSuccess) e = hipMemcpy(ctx->d_tabs, host, sizeof(Tables), hipMemcpyHostToDevice);
   free(host);
@@ -186,7 +192,14 @@ void efes_ctx_destroy(efes_ctx* ctx) {
   {
     DeviceGuard g(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    for (hipStream_t sd : ctx->side)
+      if (sd) (void)hipStreamSynchronize(sd);
     if (ctx->d_tabs) (void)hipFree(ctx->d_tabs);
+    if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
+    for (hipEvent_t ev : ctx->ev_join)
+      if (ev) (void)hipEventDestroy(ev);
+    for (hipStream_t sd : ctx->side)
+      if (sd) (void)hipStreamDestroy(sd);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   }
   delete ctx;
@@ -195,14 +208,29 @@ void efes_ctx_destroy(efes_ctx* ctx) {
 int efes_ctx_device(const efes_ctx* ctx) { return ctx ? ctx->device : -1; }
 void* efes_ctx_stream(efes_ctx* ctx) { return ctx ? static_cast<void*>(ctx->stream) : nullptr; }
 
+int efes_auto_mode(const efes_ctx* ctx, uint32_t njobs) {
+  // One wave per SIMD with the lowest per-job latency that fits: DEEP up to one
+  // job per SIMD, then grouped DEEP with 64/G jobs per wave, G = 32 .. 4; WIDE once its lanes
+  // outrun GROUP4 (which saturates at one wave per SIMD): ~2x the jobs GROUP4 holds.
+  const uint64_t simds = 4ull * (ctx ? (uint64_t)ctx->cus : 256ull), n = njobs;
+  if (n <= simds) return EFES_MODE_DEEP;
+  if (n <= 2 * simds) return EFES_MODE_GROUP32;
+  if (n <= 4 * simds) return EFES_MODE_GROUP16;
+  if (n <= 8 * simds) return EFES_MODE_GROUP8;
+  if (n <= 32 * simds) return EFES_MODE_GROUP4;
+  return EFES_MODE_WIDE;
+}
+
 int efes_hash_submit_mode(efes_ctx* ctx, const efes_job* jobs, uint32_t njobs, void* stream, int mode) {
   if (!ctx || (!jobs && njobs)) return EFES_ERR_ARG;
   if (njobs == 0) return EFES_OK;
-  if (mode == EFES_MODE_AUTO) mode = njobs <= efes::kAutoDeepMaxJobs ? EFES_MODE_DEEP : EFES_MODE_WIDE;
+  if (mode == EFES_MODE_AUTO) mode = efes_auto_mode(ctx, njobs);
   DeviceGuard g(ctx->device);
   hipStream_t s = pick(ctx, stream);
   if (mode == EFES_MODE_DEEP) return hip_err(efes::launch_deep(jobs, njobs, ctx->d_tabs, s));
   if (mode == EFES_MODE_WIDE) return hip_err(efes::launch_wide(jobs, njobs, ctx->d_tabs, s));
+  const int lanes = efes::group_of_mode(mode);
+  if (lanes) return hip_err(efes::launch_group(jobs, njobs, lanes, ctx->d_tabs, s));
   return EFES_ERR_ARG;
 }
 

@@ -36,10 +36,24 @@ efes_queue* stream_queue(efes_ctx* ctx, int* rc);
 // Launchers (host side, defined in efes_kernels.hip).
 hipError_t launch_deep(const efes_job* jobs, uint32_t njobs, const Tables* tabs, hipStream_t s);
 hipError_t launch_wide(const efes_job* jobs, uint32_t njobs, const Tables* tabs, hipStream_t s);
+// Grouped DEEP: 64/G jobs per wave, G in {4, 8, 16, 32} (64 = launch_deep).  exclusive: each
+// workgroup reserves all LDS of its CU, so no other workgroup shares the CU's SIMDs.
+hipError_t launch_group(const efes_job* jobs, uint32_t njobs, int G, const Tables* tabs, hipStream_t s,
+                        bool exclusive = false);
 hipError_t launch_fill(void* dst, size_t bytes, uint64_t seed, hipStream_t s);
 
+// Lanes per job of a grouped-DEEP mode (EFES_MODE_GROUPn -> n), 0 for other modes.
+inline int group_of_mode(int mode) {
+  switch (mode) {
+    case EFES_MODE_GROUP4: return 4;
+    case EFES_MODE_GROUP8: return 8;
+    case EFES_MODE_GROUP16: return 16;
+    case EFES_MODE_GROUP32: return 32;
+    default: return 0;
+  }
+}
+
 constexpr int kDeepWaves = 4;  // waves per DEEP workgroup: one per SIMD
-constexpr uint32_t kAutoDeepMaxJobs = 1536;  // AUTO: DEEP up to ~1.5 waves per SIMD
 
 // Makes `dev` current for the scope and restores the caller's device (C ABI calls may come
 // from any host thread, efes_hash.h).
@@ -61,6 +75,11 @@ struct DeviceGuard {
 struct efes_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  int cus = 256;                  // compute units (efes_plan_batch's capacity)
+  // side streams of a planned batch (efes_hash_submit_plan): one per part but the last
+  hipStream_t side[EFES_PLAN_MAX_PARTS - 1] = {};
+  hipEvent_t ev_fork = nullptr, ev_join[EFES_PLAN_MAX_PARTS - 1] = {};
+  std::mutex plan_mu;             // one planned submit at a time uses the side streams/events
   efes::Tables* d_tabs = nullptr;
   std::mutex mu;                  // guards the lazy creation of `digests`
   efes_queue* digests = nullptr;  // shared queue of the streaming digests (efes_stream.cpp)

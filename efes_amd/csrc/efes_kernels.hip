@@ -125,10 +125,27 @@ __device__ __forceinline__ void load_block_le(const uint8_t* src, uint32_t (&le)
 
 // ================================================================== DEEP kernel
 
+constexpr int kGroupMaxJobs = 16;  // jobs per wave in the grouped DEEP kernel (G = 4)
+
+// One job's running state between the phases of a DEEP wave (head -> bulk -> rest),
+// parked in LDS while the wave's other jobs run their phases.
+struct DeepMsg {
+  uint32_t h[5];
+  uint32_t crc_raw;
+  const uint8_t* q;  // first bulk byte (p + pos)
+  uint64_t pos;      // bytes consumed by the head
+  uint64_t nbulk;    // whole blocks after the head
+  uint64_t done;     // bulk blocks already hashed by the joint phase
+  int64_t nx_new;
+  uint32_t live;     // 0: no job, or Go panicked in the head
+  uint32_t joint;    // takes part in the grouped kernel's current joint round
+};
+
 struct DeepLDS {
   Tables tab;                                    // 36 KiB
-  uint8_t xs[kDeepWaves][64];                    // the job's tail buffer x (sha1.go:31)
+  uint8_t xs[kDeepWaves][kGroupMaxJobs][64];     // each job's tail buffer x (sha1.go:31)
   uint8_t fin[kDeepWaves][192];                  // padding assembly for checkSum
+  DeepMsg msg[kDeepWaves][kGroupMaxJobs];
 };
 
 struct DeepJob {
@@ -222,15 +239,13 @@ __device__ void deep_bulk(DeepLDS& L, int lane, const uint8_t* q, uint64_t nbulk
   }
 }
 
-__device__ void deep_job(DeepLDS& L, int wave, int lane, const DeepJob& J) {
+// Head of one Write (sha1.go:58-69): load the state, complete a pending x[:nx].  Returns the
+// job's running state; live == 0 when Go would panic (status already written).
+__device__ DeepMsg deep_head(DeepLDS& L, int lane, const DeepJob& J, uint8_t* xs) {
   const bool do_sha = J.st != nullptr, do_crc = J.cs != nullptr;
-  const bool fin = (J.flags & EFES_JOB_FINALIZE) != 0;
-  uint8_t* xs = L.xs[wave];
-  int32_t status = EFES_OK;
-
-  uint32_t h[5] = {0, 0, 0, 0, 0};
+  DeepMsg M{};
+  uint32_t (&h)[5] = M.h;
   int64_t nx = 0;
-  uint64_t len = 0;
   const bool init = (J.flags & EFES_JOB_INIT) != 0;
   if (do_sha && init) {  // NewSha1(): zero value + Reset (sha1.go:36-52)
     h[0] = kIV0; h[1] = kIV1; h[2] = kIV2; h[3] = kIV3; h[4] = kIV4;
@@ -239,20 +254,19 @@ __device__ void deep_job(DeepLDS& L, int wave, int lane, const DeepJob& J) {
 #pragma unroll
     for (int k = 0; k < 5; ++k) h[k] = uniform32(J.st->h[k]);
     nx = (int64_t)uniform64((uint64_t)J.st->nx);
-    len = uniform64(J.st->len);
     if (lane < 16) reinterpret_cast<uint32_t*>(xs)[lane] = reinterpret_cast<const uint32_t*>(J.st->x)[lane];
   }
   uint32_t crc_raw = do_crc ? (init ? 0xFFFFFFFFu : ~uniform32(J.cs->crc)) : 0u;
 
   if (do_sha && nx > 64) {  // Go: copy(d.x[d.nx:], p) panics (sha1.go:62)
     if (lane == 0 && J.status) *J.status = EFES_ERR_STATE;
-    return;
+    return M;
   }
   const uint8_t* p = J.p;
   const uint64_t plen = J.plen;
   wave_lds_sync();
 
-  // ---- head: complete the pending block x[:nx] (sha1.go:61-69)
+  // ---- complete the pending block x[:nx] (sha1.go:61-69)
   uint64_t pos = 0;
   int64_t nx_new = nx;
   if (do_sha && nx > 0) {
@@ -273,15 +287,37 @@ __device__ void deep_job(DeepLDS& L, int wave, int lane, const DeepJob& J) {
   }
   if (do_crc)
     for (uint64_t i = 0; i < pos; ++i) crc_raw = crc_byte(L.tab.slice8[0], crc_raw, ldg_u8(EFES_RANGE(p + i, 1, p, plen, "deep-crchead")));
+  M.crc_raw = crc_raw;
+  M.q = p + pos;
+  M.pos = pos;
+  M.nbulk = (plen - pos) >> 6;
+  M.done = 0;
+  M.nx_new = nx_new;
+  M.live = 1;
+  return M;
+}
 
-  // ---- bulk whole blocks (sha1.go:70-74)
-  const uint8_t* q = p + pos;
-  const uint64_t nbulk = (plen - pos) >> 6;
-  if (nbulk) {
+// The rest of one Write after the head: bulk blocks [M.done, M.nbulk) (sha1.go:70-74), the
+// tail (:75-77), Sum (:82-120) on a copy, and the write-back of state, crc, sum and status.
+__device__ void deep_rest(DeepLDS& L, int lane, const DeepJob& J, uint8_t* xs, uint8_t* fb, DeepMsg M) {
+  const bool do_sha = J.st != nullptr, do_crc = J.cs != nullptr;
+  const bool fin = (J.flags & EFES_JOB_FINALIZE) != 0;
+  int32_t status = EFES_OK;
+  uint32_t (&h)[5] = M.h;
+  uint32_t crc_raw = M.crc_raw;
+  int64_t nx_new = M.nx_new;
+  const uint8_t* p = J.p;
+  const uint64_t plen = J.plen;
+  const uint64_t pos = M.pos, nbulk = M.nbulk;
+  uint64_t len = do_sha && !(J.flags & EFES_JOB_INIT) ? uniform64(J.st->len) : 0;
+
+  // ---- bulk whole blocks not hashed yet (sha1.go:70-74)
+  if (nbulk > M.done) {
+    const uint8_t* q = M.q + 64 * M.done;
     if ((reinterpret_cast<uintptr_t>(q) & 15) == 0)
-      deep_bulk<true>(L, lane, q, nbulk, do_sha, do_crc, h, crc_raw);
+      deep_bulk<true>(L, lane, q, nbulk - M.done, do_sha, do_crc, h, crc_raw);
     else
-      deep_bulk<false>(L, lane, q, nbulk, do_sha, do_crc, h, crc_raw);
+      deep_bulk<false>(L, lane, q, nbulk - M.done, do_sha, do_crc, h, crc_raw);
   }
 
   // ---- tail (sha1.go:75-77): x[:r] = rest; x[r:] keeps stale bytes
@@ -307,7 +343,6 @@ __device__ void deep_job(DeepLDS& L, int wave, int lane, const DeepJob& J) {
     if (T & 63) {
       status = EFES_ERR_STATE;  // sha1.go:107-109 panic("d.nx != 0")
     } else {
-      uint8_t* fb = L.fin[wave];
       const uint64_t bits = len << 3;
       for (uint32_t i = lane; i < T; i += 64) {
         uint32_t b;
@@ -361,19 +396,8 @@ __device__ void deep_job(DeepLDS& L, int wave, int lane, const DeepJob& J) {
   if (lane == 0 && J.status) *J.status = status;
 }
 
-__global__ __launch_bounds__(64 * kDeepWaves, 1) void deep_kernel(const efes_job* __restrict__ jobs, uint32_t njobs,
-                                                                  const Tables* __restrict__ tabs) {
-  __shared__ __attribute__((aligned(16))) DeepLDS L;
-  {
-    const uint4* src = reinterpret_cast<const uint4*>(tabs);
-    uint4* dst = reinterpret_cast<uint4*>(&L.tab);
-    for (int i = threadIdx.x; i < (int)(sizeof(Tables) / 16); i += blockDim.x) dst[i] = src[i];
-  }
-  __syncthreads();
-  const int wave = (int)uniform32(threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  const uint32_t j = blockIdx.x * kDeepWaves + (uint32_t)wave;
-  if (j >= njobs) return;
+// Job j's descriptor as wave-uniform values.
+__device__ __forceinline__ DeepJob load_job(const efes_job* __restrict__ jobs, uint32_t j, int lane) {
   const efes_job* jb = jobs + j;
   DeepJob J;
   J.p = reinterpret_cast<const uint8_t*>(uniform64(reinterpret_cast<uint64_t>(jb->data)));
@@ -387,8 +411,190 @@ __global__ __launch_bounds__(64 * kDeepWaves, 1) void deep_kernel(const efes_job
   if (lane == 0)
     printf("EFES_CHECKED job %u p=%p len=%llu st=%p cs=%p sum=%p status=%p flags=%u\n", j, (const void*)J.p,
            (unsigned long long)J.plen, (void*)J.st, (void*)J.cs, (void*)J.sum, (void*)J.status, J.flags);
+#else
+  (void)lane;
 #endif
-  deep_job(L, wave, lane, J);
+  return J;
+}
+
+__global__ __launch_bounds__(64 * kDeepWaves, 1) void deep_kernel(const efes_job* __restrict__ jobs, uint32_t njobs,
+                                                                  const Tables* __restrict__ tabs) {
+  __shared__ __attribute__((aligned(16))) DeepLDS L;
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(tabs);
+    uint4* dst = reinterpret_cast<uint4*>(&L.tab);
+    for (int i = threadIdx.x; i < (int)(sizeof(Tables) / 16); i += blockDim.x) dst[i] = src[i];
+  }
+  __syncthreads();
+  const int wave = (int)uniform32(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const uint32_t j = blockIdx.x * kDeepWaves + (uint32_t)wave;
+  if (j >= njobs) return;
+  const DeepJob J = load_job(jobs, j, lane);
+  uint8_t* xs = L.xs[wave][0];
+  const DeepMsg M = deep_head(L, lane, J, xs);
+  if (M.live) deep_rest(L, lane, J, xs, L.fin[wave], M);
+}
+
+// ================================================================== grouped DEEP kernel
+// k = 64/G jobs per wave, G lanes (= G consecutive blocks per super-step) per job.  For
+// batches with more long jobs than SIMDs: the chain instructions are shared by the k jobs
+// (lane m*G+i runs block i of job m), so a super-step of 410 G + 770 instructions advances
+// k jobs by G blocks each: (410 G + 770)/64 instructions per block of issue work (DEEP: 422)
+// at a per-job latency of 410 + 770/G per block (WIDE: 740 at a slower issue rate).
+// DESIGN.md §4 "grouped DEEP".
+//
+// Phases per wave: the head of every job (sequential, state parked in LDS); joint rounds in
+// which the jobs with >= G bulk blocks left advance together; then, per job, the rest
+// (left-over bulk blocks through deep_bulk, tail, Sum, write-back).  Jobs are expected
+// longest-first (efes_plan_batch) so the jobs of a wave have similar lengths.
+template <int G, bool kAligned16>
+__device__ void group_bulk(DeepLDS& L, int lane, DeepMsg* msgs, uint64_t S, bool any_sha, bool any_crc) {
+  constexpr int kLG = G == 4 ? 2 : G == 8 ? 3 : G == 16 ? 4 : 5;
+  static_assert((1 << kLG) == G, "G must be 4, 8, 16 or 32");
+  const int m = lane / G, i = lane % G;
+  const DeepMsg& M = msgs[m];
+  const bool live = M.live != 0 && M.joint != 0;
+  const uint8_t* q = M.q + 64 * M.done;
+  uint32_t hv[5] = {M.h[0], M.h[1], M.h[2], M.h[3], M.h[4]}, hs[5] = {0, 0, 0, 0, 0};
+  uint32_t crc_raw = M.crc_raw;
+  uint32_t le[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) le[k] = 0;
+  if (live) load_block_le<kAligned16>(q + 64 * (uint64_t)i, le);
+  for (uint64_t st = 0; st < S; ++st) {
+    if (any_crc) {
+      uint32_t r = crc_words_raw(L.tab.slice8, 0u, le);
+#pragma unroll
+      for (int k = 0; k < kLG; ++k) {  // crc(A||B) = shift(crc(A), |B|) ^ crc(B) within the job's G lanes
+        const uint32_t o = __shfl_xor(r, 1 << k);
+        const bool right = (lane >> k) & 1;
+        r = crc_shift(L.tab.shift[k], right ? o : r) ^ (right ? r : o);
+      }
+      crc_raw = crc_shift(L.tab.shift[kLG], crc_raw) ^ r;  // running crc advanced over G*64 bytes
+    }
+    uint32_t x[80];
+    if (any_sha) {
+      uint32_t w[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) w[k] = bswap(le[k]);
+      expand_wk(w, x);
+    }
+    if (st + 1 < S) {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) le[k] = 0;
+      if (live) load_block_le<kAligned16>(q + 64 * ((st + 1) * G + (uint64_t)i), le);
+    }
+    if (any_sha) {
+      auto block = [&]() {
+        uint32_t s[5] = {hv[0], hv[1], hv[2], hv[3], hv[4]};
+        ChainRegs<0>::run(s, x);  // real in lane m*G+j of every job m at iteration j
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+          hs[k] = hv[k] + s[k];
+          hv[k] = (uint32_t)__builtin_amdgcn_mov_dpp((int)hs[k], 0x138, 0xf, 0xf, true);  // wave_shr:1
+        }
+      };
+#pragma unroll
+      for (int j = 0; j < G; j += 2) { block(); block(); }
+      // the job's chaining value is in its last lane: back to all G lanes (its first one needs it)
+#pragma unroll
+      for (int k = 0; k < 5; ++k) hv[k] = (uint32_t)__shfl((int)hs[k], lane | (G - 1));
+    }
+  }
+  wave_lds_sync();
+  if (live && i == 0) {  // joint jobs only
+    DeepMsg& W = msgs[m];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) W.h[k] = any_sha ? hv[k] : W.h[k];
+    W.crc_raw = crc_raw;
+    W.done += S * G;
+  }
+  wave_lds_sync();
+}
+
+// DeepMsg field read back from LDS as a wave-uniform value.
+__device__ __forceinline__ DeepMsg uniform_msg(const DeepMsg& s) {
+  DeepMsg M;
+#pragma unroll
+  for (int k = 0; k < 5; ++k) M.h[k] = uniform32(s.h[k]);
+  M.crc_raw = uniform32(s.crc_raw);
+  M.q = reinterpret_cast<const uint8_t*>(uniform64(reinterpret_cast<uint64_t>(s.q)));
+  M.pos = uniform64(s.pos);
+  M.nbulk = uniform64(s.nbulk);
+  M.done = uniform64(s.done);
+  M.nx_new = (int64_t)uniform64((uint64_t)s.nx_new);
+  M.live = uniform32(s.live);
+  M.joint = uniform32(s.joint);
+  return M;
+}
+
+template <int G>
+__global__ __launch_bounds__(64 * kDeepWaves, 1) void group_kernel(const efes_job* __restrict__ jobs, uint32_t njobs,
+                                                                   const Tables* __restrict__ tabs) {
+  constexpr int kJobs = 64 / G;
+  static_assert(kJobs <= kGroupMaxJobs, "LDS holds kGroupMaxJobs jobs per wave");
+  __shared__ __attribute__((aligned(16))) DeepLDS L;
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(tabs);
+    uint4* dst = reinterpret_cast<uint4*>(&L.tab);
+    for (int i = threadIdx.x; i < (int)(sizeof(Tables) / 16); i += blockDim.x) dst[i] = src[i];
+  }
+  __syncthreads();
+  const int wave = (int)uniform32(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const uint32_t j0 = (blockIdx.x * kDeepWaves + (uint32_t)wave) * kJobs;
+  if (j0 >= njobs) return;
+  DeepMsg* msgs = L.msg[wave];
+
+  // ---- heads (state parked in LDS)
+  for (int m = 0; m < kJobs; ++m) {
+    const uint32_t j = j0 + (uint32_t)m;
+    DeepMsg M{};
+    if (j < njobs) M = deep_head(L, lane, load_job(jobs, j, lane), L.xs[wave][m]);
+    wave_lds_sync();
+    if (lane == 0) msgs[m] = M;
+  }
+  wave_lds_sync();
+
+  // ---- joint rounds: while two or more jobs have >= G bulk blocks left, they advance together
+  // by S*G blocks, S = the smallest of their floor(left/G) (so a wave lasts as long as its
+  // longest job, whatever the mix of lengths); a job left alone finishes on the one-job path
+  // (422 instructions per block instead of (410 G + 770)/G).
+  for (int round = 0; round < kJobs; ++round) {
+    uint64_t S = ~0ull;
+    int joiners = 0;
+    bool any_sha = false, any_crc = false, all16 = true;
+    for (int m = 0; m < kJobs; ++m) {
+      const DeepMsg M = uniform_msg(msgs[m]);
+      const uint64_t left = M.live ? (M.nbulk - M.done) / G : 0;
+      if (left == 0) continue;
+      ++joiners;
+      S = left < S ? left : S;
+      const DeepJob J = load_job(jobs, j0 + (uint32_t)m, lane);
+      any_sha |= J.st != nullptr;
+      any_crc |= J.cs != nullptr;
+      all16 &= (reinterpret_cast<uintptr_t>(M.q + 64 * M.done) & 15) == 0;
+    }
+    if (joiners < 2) break;
+    for (int m = 0; m < kJobs; ++m) {
+      const DeepMsg M = uniform_msg(msgs[m]);
+      if (lane == 0) msgs[m].joint = M.live && (M.nbulk - M.done) / G > 0 ? 1u : 0u;
+    }
+    wave_lds_sync();
+    if (all16) group_bulk<G, true>(L, lane, msgs, S, any_sha, any_crc);
+    else group_bulk<G, false>(L, lane, msgs, S, any_sha, any_crc);
+  }
+
+  // ---- per job: left-over blocks, tail, Sum, write-back
+  for (int m = 0; m < kJobs; ++m) {
+    const uint32_t j = j0 + (uint32_t)m;
+    if (j >= njobs) break;
+    const DeepMsg M = uniform_msg(msgs[m]);
+    if (!M.live) continue;
+    const DeepJob J = load_job(jobs, j, lane);
+    deep_rest(L, lane, J, L.xs[wave][m], L.fin[wave], M);
+  }
 }
 
 // ================================================================== WIDE kernel
@@ -611,6 +817,40 @@ hipError_t launch_deep(const efes_job* jobs, uint32_t njobs, const Tables* tabs,
   const uint32_t grid = (njobs + kDeepWaves - 1) / kDeepWaves;
   hipLaunchKernelGGL(deep_kernel, dim3(grid), dim3(64 * kDeepWaves), 0, s, jobs, njobs, tabs);
   return hipGetLastError();
+}
+
+// LDS of one CU on gfx950; an exclusive launch asks for all of it per workgroup.
+constexpr size_t kCuLds = 160 * 1024;
+
+template <class K>
+hipError_t launch_reserving(K kernel, dim3 grid, dim3 block, bool exclusive, hipStream_t s, const efes_job* jobs,
+                            uint32_t njobs, const Tables* tabs) {
+  size_t dyn = 0;
+  if (exclusive) {
+    hipFuncAttributes fa{};
+    if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(kernel)) == hipSuccess && fa.sharedSizeBytes < kCuLds) {
+      dyn = kCuLds - fa.sharedSizeBytes;
+      if (hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)dyn) != hipSuccess)
+        dyn = 0;  // cannot reserve: run shared
+    }
+  }
+  hipLaunchKernelGGL(kernel, grid, block, dyn, s, jobs, njobs, tabs);
+  return hipGetLastError();
+}
+
+hipError_t launch_group(const efes_job* jobs, uint32_t njobs, int G, const Tables* tabs, hipStream_t s, bool exclusive) {
+  if (njobs == 0) return hipSuccess;
+  const uint32_t per_block = kDeepWaves * (64u / (uint32_t)G);
+  const dim3 grid((njobs + per_block - 1) / per_block), block(64 * kDeepWaves);
+  switch (G) {
+    case 4: return launch_reserving(group_kernel<4>, grid, block, exclusive, s, jobs, njobs, tabs);
+    case 8: return launch_reserving(group_kernel<8>, grid, block, exclusive, s, jobs, njobs, tabs);
+    case 16: return launch_reserving(group_kernel<16>, grid, block, exclusive, s, jobs, njobs, tabs);
+    case 32: return launch_reserving(group_kernel<32>, grid, block, exclusive, s, jobs, njobs, tabs);
+    case 64: return launch_reserving(deep_kernel, grid, block, exclusive, s, jobs, njobs, tabs);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 hipError_t launch_wide(const efes_job* jobs, uint32_t njobs, const Tables* tabs, hipStream_t s) {

@@ -21,10 +21,26 @@ import io
 import json
 import threading
 
-from ._lib import MODE_AUTO, EfesError, Sha1State, check, lib
+import numpy as np
+
+from ._lib import MODE_AUTO, EfesError, Plan, Sha1State, check, lib
 
 __all__ = ["Context", "default_context", "crc32_combine", "Sha1Digest", "CRC32Digest", "Sha1File", "Digest", "FileInfo",
            "new_sha1", "new_crc32_ieee", "EfesError"]
+
+
+def plan_batch(lengths, ctx: "Context | None" = None) -> tuple[np.ndarray, Plan]:
+    """efes_plan_batch: order[i] = index of the i-th longest job; plan = split + deep shape.
+
+    Host-only; without a context the capacity of one MI355X (1024 SIMDs) is assumed.
+    """
+    lengths = np.ascontiguousarray(lengths, dtype=np.uint64)
+    order = np.zeros(lengths.size, dtype=np.uint32)
+    plan = Plan()
+    check(lib().efes_plan_batch(ctx.handle if ctx else None, lengths.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+                                lengths.size, order.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), ctypes.byref(plan)),
+          "efes_plan_batch")
+    return order, plan
 
 
 class Context:
@@ -42,6 +58,14 @@ class Context:
 
     def submit(self, jobs_ptr: int, njobs: int, stream: int | None = None, mode: int = MODE_AUTO) -> None:
         check(lib().efes_hash_submit_mode(self.handle, jobs_ptr, njobs, stream, mode), "efes_hash_submit")
+
+    def plan(self, lengths) -> tuple[np.ndarray, Plan]:
+        """efes_plan_batch for this context's GPU: (longest-first order, plan)."""
+        return plan_batch(lengths, self)
+
+    def submit_plan(self, jobs_ptr: int, plan: Plan, stream: int | None = None) -> None:
+        """efes_hash_submit_plan: a batch laid out in plan order (DEEP part on the side stream)."""
+        check(lib().efes_hash_submit_plan(self.handle, jobs_ptr, ctypes.byref(plan), stream), "efes_hash_submit_plan")
 
     def sync(self, stream: int | None = None) -> None:
         check(lib().efes_sync(self.handle, stream), "efes_sync")

@@ -100,15 +100,54 @@ typedef struct efes_job {
 } efes_job; /* 56 bytes */
 
 /* Kernel shapes: DEEP = one wavefront per job (few, long jobs: per-job latency bound);
- * WIDE = one lane per job (many jobs: throughput bound).  AUTO picks by njobs. */
+ * WIDE = one lane per job (many jobs: throughput bound).  AUTO picks by njobs.
+ * GROUPn = grouped DEEP, 64/n jobs per wavefront with n lanes (n consecutive 64-B blocks
+ * per step) each: for more long jobs than SIMDs (lower per-job latency than WIDE, fewer
+ * instructions per byte than DEEP).  Jobs should be longest-first (efes_plan_batch).
+ * AUTO picks by njobs (efes_auto_mode). */
 #define EFES_MODE_AUTO 0
 #define EFES_MODE_DEEP 1
 #define EFES_MODE_WIDE 2
+#define EFES_MODE_GROUP4 3
+#define EFES_MODE_GROUP8 4
+#define EFES_MODE_GROUP16 5
+#define EFES_MODE_GROUP32 6
 
 /* Enqueue njobs jobs (the job array itself in DEVICE memory) on `stream` (a
  * hipStream_t; NULL = the context stream).  Asynchronous; returns launch errors only. */
 int efes_hash_submit(efes_ctx* ctx, const efes_job* jobs_device, uint32_t njobs, void* stream);
 int efes_hash_submit_mode(efes_ctx* ctx, const efes_job* jobs_device, uint32_t njobs, void* stream, int mode);
+/* The shape EFES_MODE_AUTO picks for njobs jobs of similar length (ctx may be NULL: one
+ * MI355X): DEEP up to one job per SIMD, then GROUP32..GROUP4, WIDE beyond 32 jobs per SIMD. */
+int efes_auto_mode(const efes_ctx* ctx, uint32_t njobs);
+/* Mixed-length batches (BASELINE configs[3], concurrent uploads of different sizes): the
+ * makespan is set by the longest jobs (a SHA-1 chain per job), so a batch is cut, longest
+ * first, into up to EFES_PLAN_MAX_PARTS consecutive parts that run CONCURRENTLY, each in its
+ * own kernel shape: typically the longest jobs grouped-DEEP on CUs of their own (`exclusive`:
+ * the launch reserves the CU's LDS so no other workgroup shares its SIMDs), the next ones
+ * grouped-DEEP beside the rest, which run WIDE.
+ * efes_plan_batch orders the jobs longest-first (order[i] = index into `lengths` of the job to
+ * place at jobs_device[i]) and picks the cuts, shapes and exclusivity from an issue-time model
+ * of the kernels calibrated on MI355X; efes_hash_submit_plan launches a batch
+ * laid out in that order: every part but the last on a side stream of the context, the last on
+ * `stream`, which then waits for all of them.  Planning is host-only (no device access; ctx
+ * may be NULL: then the capacity of one MI355X, 256 CUs, is assumed). */
+#define EFES_PLAN_MAX_PARTS 3
+typedef struct efes_plan_part {
+    uint32_t jobs;       /* consecutive jobs of this part (in plan order) */
+    int32_t mode;        /* EFES_MODE_DEEP, EFES_MODE_GROUPn or EFES_MODE_WIDE */
+    uint32_t exclusive;  /* 1: workgroups reserve their CU (DEEP/GROUPn only) */
+    uint32_t _reserved;
+} efes_plan_part;
+typedef struct efes_plan {
+    uint32_t njobs;      /* jobs in the batch = sum of part[i].jobs */
+    uint32_t nparts;     /* parts in use, 1..EFES_PLAN_MAX_PARTS (0 for an empty batch) */
+    efes_plan_part part[EFES_PLAN_MAX_PARTS];
+    double est_seconds;  /* the model's makespan estimate (informational) */
+} efes_plan;
+int efes_plan_batch(efes_ctx* ctx, const uint64_t* lengths, uint32_t n, uint32_t* order, efes_plan* plan);
+int efes_hash_submit_plan(efes_ctx* ctx, const efes_job* jobs_device, const efes_plan* plan, void* stream);
+
 /* Wait for `stream` (NULL = context stream); reports latched asynchronous errors. */
 int efes_sync(efes_ctx* ctx, void* stream);
 

@@ -27,11 +27,15 @@ def env():
                 ctx=ctx)
 
 
-MODE_IDS = ["deep", "wide"]
+MODE_IDS = ["deep", "wide", "group4", "group8", "group16", "group32", "plan"]
 
 
 def _modes(env):
-    return {"deep": env["efes"].MODE_DEEP, "wide": env["efes"].MODE_WIDE}
+    from efes_amd._lib import MODE_GROUP
+    from efes_amd.batch import MODE_PLAN
+    m = {"deep": env["efes"].MODE_DEEP, "wide": env["efes"].MODE_WIDE, "plan": MODE_PLAN}
+    m.update({f"group{g}": v for g, v in MODE_GROUP.items()})
+    return m
 
 
 def device_buffer(env, host: np.ndarray):
@@ -230,7 +234,7 @@ def test_zero_jobs(env):
     env["ctx"].sync()
 
 
-def test_many_small_jobs_auto_wide(env, oracle):
+def test_many_small_jobs_auto(env, oracle):
     rng = np.random.default_rng(2)
     n = 5000
     lengths = rng.integers(0, 3000, n)
@@ -238,7 +242,7 @@ def test_many_small_jobs_auto_wide(env, oracle):
     host = oracle.fill_synthetic(int(lengths.sum()) + 8, 1234)
     buf = device_buffer(env, host)
     b = env["DeviceBatch"](buf.data_ptr(), offsets, lengths, ctx=env["ctx"])
-    b.run()  # AUTO -> WIDE at this count
+    b.run()  # AUTO -> GROUP16 at this count (efes_auto_mode)
     assert (b.status_host() == 0).all()
     shas, crcs = b.sha1_hex(), b.crc_sum()
     for i in range(0, n, 7):
@@ -289,6 +293,7 @@ def test_device_fill_matches_host_generator(env, oracle):
     for n, seed in [(8, 1), (1000, 2), (4097, 3), (1 << 20, 0xEFE5)]:
         buf = torch.zeros(n + 8, dtype=torch.uint8, device="cuda:0")
         env["ctx"].fill_synthetic(buf.data_ptr(), n, seed, torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()  # a null-stream handle selects the context's own non-blocking stream
         got = buf.cpu().numpy()
         assert got[:n].tobytes() == oracle.fill_synthetic(n, seed).tobytes()
         assert not got[n:].any()
@@ -729,3 +734,57 @@ def test_host_ingest_zero_copy(env, oracle):
     with pytest.raises(env["efes"].EfesError) as e:
         hb.run(EFES_HOST_ZERO_COPY)
     assert e.value.code == env["efes"].EFES_ERR_ARG
+
+
+@pytest.mark.parametrize("lanes", [4, 8, 16, 32])
+def test_group_joint_phase_mixed_lengths_and_states(env, oracle, lanes):
+    """Grouped DEEP: jobs of one wave with different lengths, offsets and mid-stream states.
+
+    Lengths are long enough for the joint phase (S > 0) and leave per-job left-over blocks,
+    heads (nx != 0) and tails; some waves mix in short jobs that the cost model keeps out of
+    the joint phase.  Wave j holds jobs [j*64/lanes, (j+1)*64/lanes)."""
+    from efes_amd._lib import MODE_GROUP
+    rng = np.random.default_rng(lanes)
+    n = 3 * (64 // lanes) + 5  # three full waves and a partial one
+    lengths = []
+    for i in range(n):
+        if i % 7 == 3:
+            lengths.append(int(rng.integers(0, 200)))
+        else:
+            lengths.append(int(rng.integers(40, 120)) * 64 * lanes + int(rng.integers(0, 130)))
+    offsets, pos = [], 0
+    for L in lengths:
+        pos += int(rng.integers(0, 40))
+        offsets.append(pos)
+        pos += L
+    host = oracle.fill_synthetic(pos + 64, 4242 + lanes)
+    buf = device_buffer(env, host)
+    states, crcs = midstream_states(oracle, env, n, random.Random(lanes))
+    b = env["DeviceBatch"](buf.data_ptr(), offsets, lengths, states=states, crcs=crcs, ctx=env["ctx"])
+    b.run(MODE_GROUP[lanes])
+    datas = [host[o:o + L].tobytes() for o, L in zip(offsets, lengths)]
+    check_batch(b, oracle, datas, states, crcs, what=f"group{lanes}")
+
+
+@pytest.mark.parametrize("force", ["4:40x", "8:24", "16:10x,4:30", "32:6,8:20", "64:3x", "0:0", "16:1000",
+                                   "64:2x,32:4"])
+def test_planned_batch_forced_parts(env, oracle, force, monkeypatch):
+    """efes_hash_submit_plan: parts on side streams + the caller's stream, concurrently, some
+    of them exclusive (CU-reserving LDS) -- every job lands in exactly one launch."""
+    from efes_amd.batch import MODE_PLAN
+    rng = np.random.default_rng(5)
+    n = 150
+    lengths = (np.asarray([64 << 10 << int(k) for k in rng.integers(0, 5, n)]) // 16 + rng.integers(0, 100, n))
+    offsets = np.concatenate([[0], np.cumsum(lengths)[:-1]]).astype(np.uint64)
+    host = oracle.fill_synthetic(int(lengths.sum()) + 8, 77)
+    buf = device_buffer(env, host)
+    monkeypatch.setenv("EFES_PLAN_FORCE", force)
+    b = env["DeviceBatch"](buf.data_ptr(), offsets, lengths, fresh=True, ctx=env["ctx"])
+    b.make_plan()
+    assert sum(p[0] for p in b.plan.parts()) == n
+    b.run(MODE_PLAN)
+    assert (b.status_host() == 0).all()
+    shas, crcs = b.sha1_hex(), b.crc_sum()
+    for i in range(n):
+        dat = host[int(offsets[i]):int(offsets[i]) + int(lengths[i])].tobytes()
+        assert shas[i] == hashlib.sha1(dat).hexdigest() and crcs[i] == zlib.crc32(dat), (force, i)

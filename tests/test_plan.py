@@ -1,0 +1,89 @@
+"""Host logic of efes_plan_batch (no GPU: planning is host-only, ctx = NULL assumes one MI355X).
+
+The planner orders a batch longest-first and splits it between a DEEP / grouped-DEEP launch
+(the long jobs) and a WIDE launch (the rest) by an issue-time model (efes_plan.cpp)."""
+import numpy as np
+import pytest
+
+from efes_amd._lib import MODE_DEEP, MODE_GROUP, MODE_WIDE
+from efes_amd.hashing import plan_batch
+
+MiB = 1 << 20
+
+
+def test_order_is_stable_longest_first():
+    rng = np.random.default_rng(1)
+    lengths = rng.integers(0, 5, 1000).astype(np.uint64) * 4096
+    order, plan = plan_batch(lengths)
+    assert sorted(order.tolist()) == list(range(1000))
+    got = lengths[order]
+    assert (np.diff(got.astype(np.int64)) <= 0).all()
+    for v in np.unique(lengths):  # stable within equal lengths
+        idx = order[got == v]
+        assert (np.diff(idx.astype(np.int64)) > 0).all()
+    assert plan.njobs == 1000 and sum(p[0] for p in plan.parts()) == 1000
+
+
+def test_metric_config_goes_deep():
+    """BASELINE configs[1]/[2]: 1024 x 4 MiB = one job per SIMD -> all DEEP (one wave per job)."""
+    _, plan = plan_batch([4 * MiB] * 1024)
+    assert [(j, m) for j, m, _ in plan.parts()] == [(1024, MODE_DEEP)]
+
+
+def test_ingest_config_goes_wide():
+    """BASELINE configs[4] per launch: 131072 x 4 MiB -> throughput-bound, all WIDE."""
+    _, plan = plan_batch([4 * MiB] * 131072)
+    assert plan.parts() == [(131072, MODE_WIDE, False)]
+
+
+def test_mixed_config_splits_longest_class_off():
+    """BASELINE configs[3]: ChunkSize 64K..64M -> the longest classes grouped-DEEP on CUs of
+    their own, the rest WIDE on the other CUs."""
+    sizes = np.asarray([64 << 10 << i for i in range(11)], dtype=np.uint64)
+    lengths = sizes[np.random.default_rng(7).integers(0, 11, 65536)]
+    order, plan = plan_batch(lengths)
+    parts = plan.parts()
+    assert len(parts) in (2, 3) and sum(p[0] for p in parts) == 65536
+    for jobs, mode, exclusive in parts[:-1]:  # grouped DEEP on CUs of their own
+        assert mode in MODE_GROUP.values() and exclusive
+    assert parts[-1][1] == MODE_WIDE and not parts[-1][2]
+    # cuts fall between lengths: every job of a part is at least as long as every later one
+    cut = 0
+    for jobs, _, _ in parts[:-1]:
+        cut += jobs
+        assert lengths[order[cut - 1]] > lengths[order[cut]]
+    assert lengths[order[0]] == 64 * MiB
+    assert 0.5 < plan.est_seconds < 2.0
+
+
+def test_more_long_jobs_than_simds_use_groups():
+    _, plan = plan_batch([4 * MiB] * 4096)
+    assert len(plan.parts()) == 1 and plan.parts()[0][1] in MODE_GROUP.values()
+
+
+def test_empty_and_zero_lengths():
+    order, plan = plan_batch([])
+    assert plan.njobs == 0 and plan.nparts == 0 and order.size == 0
+    order, plan = plan_batch([0, 0, 0])
+    assert plan.njobs == 3 and sorted(order.tolist()) == [0, 1, 2] and sum(p[0] for p in plan.parts()) == 3
+
+
+@pytest.mark.parametrize("force,expect", [
+    ("8:100", [(100, MODE_GROUP[8], False), (2900, MODE_WIDE, False)]),
+    ("64:5000", [(3000, MODE_DEEP, False)]),
+    ("4:10x,16:20", [(10, MODE_GROUP[4], True), (20, MODE_GROUP[16], False), (2970, MODE_WIDE, False)]),
+    ("0:3000", [(3000, MODE_WIDE, False)]),
+    ("0:5x", [(5, MODE_WIDE, False), (2995, MODE_WIDE, False)]),
+])
+def test_force_override(monkeypatch, force, expect):
+    monkeypatch.setenv("EFES_PLAN_FORCE", force)
+    _, plan = plan_batch([MiB] * 3000)
+    assert plan.parts() == expect
+
+
+def test_force_override_rejects_too_many_parts(monkeypatch):
+    """A forced plan that would need a fourth part is ignored (the model's plan stands)."""
+    _, model = plan_batch([MiB] * 3000)
+    monkeypatch.setenv("EFES_PLAN_FORCE", "4:10,8:10,16:10")
+    _, plan = plan_batch([MiB] * 3000)
+    assert plan.parts() == model.parts()

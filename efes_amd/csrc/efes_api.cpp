@@ -211,13 +211,13 @@ void* efes_ctx_stream(efes_ctx* ctx) { return ctx ? static_cast<void*>(ctx->stre
 int efes_auto_mode(const efes_ctx* ctx, uint32_t njobs) {
   // One wave per SIMD with the lowest per-job latency that fits: DEEP up to one
   // job per SIMD, then grouped DEEP with 64/G jobs per wave, G = 32 .. 4; WIDE once its lanes
-  // outrun GROUP4 (which saturates at one wave per SIMD): ~2x the jobs GROUP4 holds.
+  // outrun GROUP4 (which saturates at one wave per SIMD, ~1 TB/s): WIDE lanes at ~40 MB/s each.
   const uint64_t simds = 4ull * (ctx ? (uint64_t)ctx->cus : 256ull), n = njobs;
   if (n <= simds) return EFES_MODE_DEEP;
   if (n <= 2 * simds) return EFES_MODE_GROUP32;
   if (n <= 4 * simds) return EFES_MODE_GROUP16;
   if (n <= 8 * simds) return EFES_MODE_GROUP8;
-  if (n <= 32 * simds) return EFES_MODE_GROUP4;
+  if (n <= 24 * simds) return EFES_MODE_GROUP4;
   return EFES_MODE_WIDE;
 }
 

@@ -616,48 +616,115 @@ __device__ __forceinline__ uint32_t fin_byte(const uint8_t* xl, uint32_t i, uint
   return 0u;
 }
 
-__device__ __forceinline__ void sha_block(const uint32_t (&le)[16], uint32_t (&h)[5]) {
-  uint32_t w[16];
-#pragma unroll
-  for (int k = 0; k < 16; ++k) w[k] = bswap(le[k]);
-  compress_inline(h, w);
-}
-
 // Whole blocks of one lane's message, software-pipelined: the next block is in flight while
 // the current one is compressed (a lone uncoalesced 64-B load per lane would otherwise expose
 // the full memory latency every block).  kSha/kCrc are wave-uniform template flags, so CRC
 // lookups and SHA-1 rounds share one basic block; a lane that needs only one of the two
 // computes both and never stores the other.  Lanes run their own trip counts; with jobs
 // sorted by length the lanes of a wave finish together.
-template <bool kAligned16, bool kSha, bool kCrc>
-__device__ __forceinline__ void wide_bulk(const uint8_t* q, uint64_t nbulk, const uint32_t (&t)[8][256],
-                                          uint32_t (&h)[5], uint32_t& crc_raw) {
-  // Skewed: each step compresses block b and CRCs block b+1, two chains with no data
-  // dependence on each other, so a lone wave (configs 3/4 run 1-2 waves per SIMD) has
-  // independent work to issue while either chain waits on its latency.
-  uint32_t A[16], B[16];
-  if (nbulk == 0) return;
-  load_block_le<kAligned16>(q, A);
-  if (nbulk > 1) load_block_le<kAligned16>(q + 64, B);
-  if constexpr (kCrc) crc_raw = crc_words_raw(t, crc_raw, A);
-  for (uint64_t b = 0; b < nbulk; b += 2) {
-    if constexpr (kSha) sha_block(A, h);
-    if (b + 1 >= nbulk) break;
-    if constexpr (kCrc) crc_raw = crc_words_raw(t, crc_raw, B);
-    if (b + 2 < nbulk) load_block_le<kAligned16>(q + 64 * (b + 2), A);
-    if constexpr (kSha) sha_block(B, h);
-    if (b + 2 >= nbulk) break;
-    if constexpr (kCrc) crc_raw = crc_words_raw(t, crc_raw, A);
-    if (b + 3 < nbulk) load_block_le<kAligned16>(q + 64 * (b + 3), B);
-  }
+
+// One slicing-by-8 step (8 bytes = LE words 2S, 2S+1) of crc_words_raw, split in two: the eight
+// table lookups are issued first, the XORs that consume them come five SHA-1 rounds later.
+struct CrcPending {
+  uint32_t v[8];
+};
+template <int S>
+__device__ __forceinline__ void crc_issue(const uint32_t (&t)[8][256], uint32_t crc, const uint32_t (&le)[16],
+                                          CrcPending& p) {
+  const uint32_t hi = le[2 * S + 1];
+  const uint32_t c = crc ^ le[2 * S];
+  p.v[0] = t[0][hi >> 24]; p.v[1] = t[1][(hi >> 16) & 0xffu]; p.v[2] = t[2][(hi >> 8) & 0xffu];
+  p.v[3] = t[3][hi & 0xffu]; p.v[4] = t[4][c >> 24]; p.v[5] = t[5][(c >> 16) & 0xffu];
+  p.v[6] = t[6][(c >> 8) & 0xffu]; p.v[7] = t[7][c & 0xffu];
+}
+__device__ __forceinline__ uint32_t crc_combine(const CrcPending& p) {
+  const uint32_t a = __builtin_amdgcn_bitop3_b32(p.v[0], p.v[1], p.v[2], 0x96);
+  const uint32_t b = __builtin_amdgcn_bitop3_b32(p.v[3], p.v[4], p.v[5], 0x96);
+  return __builtin_amdgcn_bitop3_b32(a, b, p.v[6] ^ p.v[7], 0x96);
 }
 
+// 80 inline SHA-1 rounds with the 8 CRC steps of the same block woven in: step k's lookups are
+// issued after round 10k+4 and combined after round 10k+9, so the LDS latency of the CRC's
+// dependent lookups is covered by SHA-1 rounds.  Scheduling barriers every five rounds keep
+// the compiler from regrouping the CRC steps into back-to-back lookup/wait clusters.
+template <int R, bool kSha, bool kCrc>
+struct WideRounds {
+  __device__ __forceinline__ static void run(uint32_t (&s)[5], uint32_t (&w)[16], const uint32_t (&t)[8][256],
+                                             uint32_t& crc, const uint32_t (&le)[16], CrcPending& p) {
+    if constexpr (kSha) round_inline<R>(s, w);
+    if constexpr (kCrc && R % 10 == 4) crc_issue<R / 10>(t, crc, le, p);
+    if constexpr (kCrc && R % 10 == 9) crc = crc_combine(p);
+    if constexpr (kSha && kCrc && R % 5 == 4) __builtin_amdgcn_sched_barrier(0);
+    WideRounds<R + 1, kSha, kCrc>::run(s, w, t, crc, le, p);
+  }
+};
+template <bool kSha, bool kCrc>
+struct WideRounds<80, kSha, kCrc> {
+  __device__ __forceinline__ static void run(uint32_t (&)[5], uint32_t (&)[16], const uint32_t (&)[8][256], uint32_t&,
+                                             const uint32_t (&)[16], CrcPending&) {}
+};
+
+// One block of one lane's message; `live` lanes (b < their own block count) commit the result.
+template <bool kSha, bool kCrc>
+__device__ __forceinline__ void wide_step(const uint32_t (&le)[16], const uint32_t (&t)[8][256], uint32_t (&h)[5],
+                                          uint32_t& crc_raw, bool live) {
+  uint32_t w[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) w[k] = bswap(le[k]);
+  uint32_t s[5] = {h[0], h[1], h[2], h[3], h[4]};
+  uint32_t c = crc_raw;
+  CrcPending p;
+  WideRounds<0, kSha, kCrc>::run(s, w, t, c, le, p);
+  if constexpr (kSha) {
+#pragma unroll
+    for (int k = 0; k < 5; ++k) h[k] = live ? h[k] + s[k] : h[k];
+  }
+  if constexpr (kCrc) crc_raw = live ? c : crc_raw;
+}
+
+// Whole blocks of one lane's message: block b is hashed (SHA-1 rounds and CRC steps woven
+// together) while blocks b+1 and b+2 are in flight (three 16-word buffers, loop unrolled by
+// three so the buffers keep their registers).  The trip count is the wave's longest message
+// (`nmax`, uniform), so the loads are unconditional and the compiler's vmcnt waits are exact;
+// lanes past their own last block load a harmless `dummy` block and do not commit.  kSha/kCrc
+// are wave-uniform template flags; a lane that needs only one of the two computes both and
+// never stores the other.  Jobs sorted by length keep the lanes of a wave equally long.
+template <bool kAligned16, bool kSha, bool kCrc>
+__device__ __forceinline__ void wide_bulk(const uint8_t* q, uint64_t nbulk, uint64_t nmax, const uint8_t* dummy,
+                                          const uint32_t (&t)[8][256], uint32_t (&h)[5], uint32_t& crc_raw) {
+  auto src = [&](uint64_t b) { return b < nbulk ? q + 64 * b : dummy; };
+  uint32_t A[16], B[16], C[16];
+  if (nmax == 0) return;
+  load_block_le<kAligned16>(src(0), A);
+  load_block_le<kAligned16>(src(1), B);
+  for (uint64_t b = 0; b < nmax; b += 3) {
+    load_block_le<kAligned16>(src(b + 2), C);
+    wide_step<kSha, kCrc>(A, t, h, crc_raw, b < nbulk);
+    if (b + 1 >= nmax) break;
+    load_block_le<kAligned16>(src(b + 3), A);
+    wide_step<kSha, kCrc>(B, t, h, crc_raw, b + 1 < nbulk);
+    if (b + 2 >= nmax) break;
+    load_block_le<kAligned16>(src(b + 4), B);
+    wide_step<kSha, kCrc>(C, t, h, crc_raw, b + 2 < nbulk);
+  }
+}
 template <bool kAligned16>
-__device__ __forceinline__ void wide_bulk_any(const uint8_t* q, uint64_t nbulk, bool any_sha, bool any_crc,
-                                              const uint32_t (&t)[8][256], uint32_t (&h)[5], uint32_t& crc_raw) {
-  if (any_sha && any_crc) wide_bulk<kAligned16, true, true>(q, nbulk, t, h, crc_raw);
-  else if (any_sha) wide_bulk<kAligned16, true, false>(q, nbulk, t, h, crc_raw);
-  else if (any_crc) wide_bulk<kAligned16, false, true>(q, nbulk, t, h, crc_raw);
+__device__ __forceinline__ void wide_bulk_any(const uint8_t* q, uint64_t nbulk, uint64_t nmax, const uint8_t* dummy,
+                                              bool any_sha, bool any_crc, const uint32_t (&t)[8][256],
+                                              uint32_t (&h)[5], uint32_t& crc_raw) {
+  if (any_sha && any_crc) wide_bulk<kAligned16, true, true>(q, nbulk, nmax, dummy, t, h, crc_raw);
+  else if (any_sha) wide_bulk<kAligned16, true, false>(q, nbulk, nmax, dummy, t, h, crc_raw);
+  else if (any_crc) wide_bulk<kAligned16, false, true>(q, nbulk, nmax, dummy, t, h, crc_raw);
+}
+
+// Wave-wide maximum of a per-lane 64-bit value (uniform result).
+__device__ __forceinline__ uint64_t wave_max64(uint64_t v) {
+#pragma unroll
+  for (int k = 1; k < 64; k <<= 1) {
+    const uint64_t o = (uint64_t)__shfl_xor((unsigned long long)v, k);
+    v = o > v ? o : v;
+  }
+  return uniform64(v);
 }
 
 __global__ __launch_bounds__(64 * kWideWaves, 2) void wide_kernel(const efes_job* __restrict__ jobs, uint32_t njobs,
@@ -730,8 +797,10 @@ __global__ __launch_bounds__(64 * kWideWaves, 2) void wide_kernel(const efes_job
   const uint64_t nbulk = go ? (plen - pos) >> 6 : 0;
   const bool all16 = __all(!go || (reinterpret_cast<uintptr_t>(q) & 15) == 0);
   const bool any_sha = __any(do_sha), any_crc = __any(do_crc);  // wave-uniform
-  if (all16) wide_bulk_any<true>(q, nbulk, any_sha, any_crc, L.slice8, h, crc_raw);
-  else wide_bulk_any<false>(q, nbulk, any_sha, any_crc, L.slice8, h, crc_raw);
+  const uint64_t nmax = wave_max64(nbulk);
+  const uint8_t* dummy = reinterpret_cast<const uint8_t*>(tabs);  // 36 KiB of valid device memory
+  if (all16) wide_bulk_any<true>(q, nbulk, nmax, dummy, any_sha, any_crc, L.slice8, h, crc_raw);
+  else wide_bulk_any<false>(q, nbulk, nmax, dummy, any_sha, any_crc, L.slice8, h, crc_raw);
 
   // ---- tail
   const uint64_t tpos = pos + (nbulk << 6);

@@ -7,7 +7,7 @@
 //   shape                      latency of one job           SIMD work per job
 //   DEEP  (one wave per job)   422 x 4.1                    422 x 4.1
 //   GROUPn (64/n jobs / wave)  (410 + 770/n) x 4.1          (410 n + 770)/64 x 4.1
-//   WIDE  (one lane per job)   740 x 6.8                    740/64 x 6.8 (/1.41 once SIMDs hold 2+ waves)
+//   WIDE  (one lane per job)   740 x 5.1                    740/64 x 5.1 (/1.06 once SIMDs hold 2+ waves)
 // A DEEP/GROUP wave issues at ~4.1 cycles per instruction alone and gains almost nothing from
 // a second wave on its SIMD (1.06x), so where a long job's wave lands matters: the plan can
 // give the longest jobs CUs of their own (exclusive launch) and run the rest on the others.
@@ -34,8 +34,8 @@
 namespace {
 
 constexpr double kCpiDeep = 4.1;    // cycles per instruction, DEEP / GROUP wave alone
-constexpr double kCpiWide = 6.8;    // cycles per instruction, WIDE wave alone (LDS lookups, 64-B lane loads)
-constexpr double kWideShare = 1.41; // WIDE throughput of a SIMD holding two waves vs one
+constexpr double kCpiWide = 5.1;    // cycles per instruction, WIDE wave alone (dependent CRC LDS lookups)
+constexpr double kWideShare = 1.06; // WIDE throughput of a SIMD holding two waves vs one
 constexpr double kClock = 2.36e9;   // Hz (GRBM_GUI_ACTIVE during DEEP), for est_seconds only
 constexpr int kWideLanes = 0;       // "shape" id of WIDE in the search
 

@@ -118,7 +118,7 @@ typedef struct efes_job {
 int efes_hash_submit(efes_ctx* ctx, const efes_job* jobs_device, uint32_t njobs, void* stream);
 int efes_hash_submit_mode(efes_ctx* ctx, const efes_job* jobs_device, uint32_t njobs, void* stream, int mode);
 /* The shape EFES_MODE_AUTO picks for njobs jobs of similar length (ctx may be NULL: one
- * MI355X): DEEP up to one job per SIMD, then GROUP32..GROUP4, WIDE beyond 32 jobs per SIMD. */
+ * MI355X): DEEP up to one job per SIMD, then GROUP32..GROUP4, WIDE beyond 24 jobs per SIMD. */
 int efes_auto_mode(const efes_ctx* ctx, uint32_t njobs);
 /* Mixed-length batches (BASELINE configs[3], concurrent uploads of different sizes): the
  * makespan is set by the longest jobs (a SHA-1 chain per job), so a batch is cut, longest

@@ -9,17 +9,19 @@
 // included, so MarshalText (sha1_efes.go:25-38) of a device state equals Go's.
 //
 // Two kernel shapes:
-//   DEEP: one wavefront per job.  SHA-1 is a strict chain of 64-byte compressions, so a
-//         job's speed is one wave's issue rate.  The 64 lanes load 64 consecutive blocks
-//         (4 KiB, coalesced), compute their CRC-32 partials and expand their message
-//         schedules W[i]+K[i] into their own registers; the per-block CRCs are combined by
-//         a 6-level GF(2) shift tree; then the 80-round chain of block i runs in lane i
-//         (5 VALU per round, W+K from registers) and the chaining value steps to lane i+1
-//         by DPP: 405 chain VALU + 5 DPP moves per block.
+//   DEEP: one chain wavefront per job.  SHA-1 is a strict chain of 64-byte compressions, so a
+//         job's speed is one wave's issue rate.  A producer wave on the same SIMD loads 64
+//         consecutive blocks (4 KiB, coalesced), computes their CRC-32 partials (combined by a
+//         6-level GF(2) shift tree) and expands each block's schedule W[i]+K[i]; the chain wave
+//         copies its lane's block W+K from LDS into registers, the 80-round chain of block i
+//         runs in lane i (5 VALU per round) and the chaining value steps to lane i+1 by DPP:
+//         405 chain VALU + 5 DPP moves per block.
+//   GROUPn: 64/n jobs per wavefront (n lanes each), the DEEP chain shared by the jobs.
 //   WIDE: one lane per job (64 jobs per wave), schedule inline, CRC fused per lane.
 //         Throughput shape for many concurrent jobs.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "efes_internal.hpp"
@@ -169,7 +171,7 @@ struct DeepJob {
 // per block).  Measured against W+K read back from LDS by ds_read_b128: 48.1 vs 52.7 ms per
 // 1024 x 4 MiB.
 template <bool kAligned16>
-__device__ void deep_bulk(DeepLDS& L, int lane, const uint8_t* q, uint64_t nbulk, bool do_sha, bool do_crc,
+__device__ void deep_bulk(const Tables& T, int lane, const uint8_t* q, uint64_t nbulk, bool do_sha, bool do_crc,
                           uint32_t (&h)[5], uint32_t& crc_raw) {
   uint32_t le[16];
   // Blocks are right-aligned in the lanes (lane 64-nb+i holds block i) so that the zero
@@ -184,19 +186,19 @@ __device__ void deep_bulk(DeepLDS& L, int lane, const uint8_t* q, uint64_t nbulk
   }
   while (b0 < nbulk) {
     if (do_crc) {
-      uint32_t r = crc_words_raw(L.tab.slice8, 0u, le);  // raw CRC of this lane's block, register 0
+      uint32_t r = crc_words_raw(T.slice8, 0u, le);  // raw CRC of this lane's block, register 0
 #pragma unroll
       for (int k = 0; k < 6; ++k) {  // crc(A||B) = shift(crc(A), |B|) ^ crc(B), |B| = 64<<k bytes
         const uint32_t o = __shfl_xor(r, 1 << k);
         const bool right = (lane >> k) & 1;
-        r = crc_shift(L.tab.shift[k], right ? o : r) ^ (right ? r : o);
+        r = crc_shift(T.shift[k], right ? o : r) ^ (right ? r : o);
       }
       if (nb == 64) {
-        crc_raw = crc_shift(L.tab.shift[6], crc_raw);
+        crc_raw = crc_shift(T.shift[6], crc_raw);
       } else {
 #pragma unroll
         for (int k = 0; k < 6; ++k)
-          if ((nb >> k) & 1) crc_raw = crc_shift(L.tab.shift[k], crc_raw);
+          if ((nb >> k) & 1) crc_raw = crc_shift(T.shift[k], crc_raw);
       }
       crc_raw ^= r;
     }
@@ -241,7 +243,7 @@ __device__ void deep_bulk(DeepLDS& L, int lane, const uint8_t* q, uint64_t nbulk
 
 // Head of one Write (sha1.go:58-69): load the state, complete a pending x[:nx].  Returns the
 // job's running state; live == 0 when Go would panic (status already written).
-__device__ DeepMsg deep_head(DeepLDS& L, int lane, const DeepJob& J, uint8_t* xs) {
+__device__ DeepMsg deep_head(const Tables& T, int lane, const DeepJob& J, uint8_t* xs) {
   const bool do_sha = J.st != nullptr, do_crc = J.cs != nullptr;
   DeepMsg M{};
   uint32_t (&h)[5] = M.h;
@@ -286,7 +288,7 @@ __device__ DeepMsg deep_head(DeepLDS& L, int lane, const DeepJob& J, uint8_t* xs
     pos = nh;
   }
   if (do_crc)
-    for (uint64_t i = 0; i < pos; ++i) crc_raw = crc_byte(L.tab.slice8[0], crc_raw, ldg_u8(EFES_RANGE(p + i, 1, p, plen, "deep-crchead")));
+    for (uint64_t i = 0; i < pos; ++i) crc_raw = crc_byte(T.slice8[0], crc_raw, ldg_u8(EFES_RANGE(p + i, 1, p, plen, "deep-crchead")));
   M.crc_raw = crc_raw;
   M.q = p + pos;
   M.pos = pos;
@@ -299,7 +301,7 @@ __device__ DeepMsg deep_head(DeepLDS& L, int lane, const DeepJob& J, uint8_t* xs
 
 // The rest of one Write after the head: bulk blocks [M.done, M.nbulk) (sha1.go:70-74), the
 // tail (:75-77), Sum (:82-120) on a copy, and the write-back of state, crc, sum and status.
-__device__ void deep_rest(DeepLDS& L, int lane, const DeepJob& J, uint8_t* xs, uint8_t* fb, DeepMsg M) {
+__device__ void deep_rest(const Tables& T, int lane, const DeepJob& J, uint8_t* xs, uint8_t* fb, DeepMsg M) {
   const bool do_sha = J.st != nullptr, do_crc = J.cs != nullptr;
   const bool fin = (J.flags & EFES_JOB_FINALIZE) != 0;
   int32_t status = EFES_OK;
@@ -315,16 +317,16 @@ __device__ void deep_rest(DeepLDS& L, int lane, const DeepJob& J, uint8_t* xs, u
   if (nbulk > M.done) {
     const uint8_t* q = M.q + 64 * M.done;
     if ((reinterpret_cast<uintptr_t>(q) & 15) == 0)
-      deep_bulk<true>(L, lane, q, nbulk - M.done, do_sha, do_crc, h, crc_raw);
+      deep_bulk<true>(T, lane, q, nbulk - M.done, do_sha, do_crc, h, crc_raw);
     else
-      deep_bulk<false>(L, lane, q, nbulk - M.done, do_sha, do_crc, h, crc_raw);
+      deep_bulk<false>(T, lane, q, nbulk - M.done, do_sha, do_crc, h, crc_raw);
   }
 
   // ---- tail (sha1.go:75-77): x[:r] = rest; x[r:] keeps stale bytes
   const uint64_t tpos = pos + (nbulk << 6);
   const uint32_t r = (uint32_t)(plen - tpos);
   if (do_crc)
-    for (uint32_t i = 0; i < r; ++i) crc_raw = crc_byte(L.tab.slice8[0], crc_raw, ldg_u8(EFES_RANGE(p + tpos + i, 1, p, plen, "deep-crctail")));
+    for (uint32_t i = 0; i < r; ++i) crc_raw = crc_byte(T.slice8[0], crc_raw, ldg_u8(EFES_RANGE(p + tpos + i, 1, p, plen, "deep-crctail")));
   if (do_sha && r > 0) {
     if ((uint32_t)lane < r) xs[lane] = ldg_u8(EFES_RANGE(p + tpos + lane, 1, p, plen, "deep-tail"));
     nx_new = r;
@@ -417,23 +419,195 @@ __device__ __forceinline__ DeepJob load_job(const efes_job* __restrict__ jobs, u
   return J;
 }
 
-__global__ __launch_bounds__(64 * kDeepWaves, 1) void deep_kernel(const efes_job* __restrict__ jobs, uint32_t njobs,
+// DeepMsg field read back from LDS as a wave-uniform value.
+__device__ __forceinline__ DeepMsg uniform_msg(const DeepMsg& s) {
+  DeepMsg M;
+#pragma unroll
+  for (int k = 0; k < 5; ++k) M.h[k] = uniform32(s.h[k]);
+  M.crc_raw = uniform32(s.crc_raw);
+  M.q = reinterpret_cast<const uint8_t*>(uniform64(reinterpret_cast<uint64_t>(s.q)));
+  M.pos = uniform64(s.pos);
+  M.nbulk = uniform64(s.nbulk);
+  M.done = uniform64(s.done);
+  M.nx_new = (int64_t)uniform64((uint64_t)s.nx_new);
+  M.live = uniform32(s.live);
+  M.joint = uniform32(s.joint);
+  return M;
+}
+
+// ================================================================== DEEP kernel, producer/consumer
+// Workgroup = 4 chain waves + 4 producer waves; wave w+4 always lands on the same SIMD as wave
+// w (tools/microbench/mb_placement.hip), so each SIMD hosts one job's chain and its producer.
+// The producer does everything of a super-step that is not the chain -- the coalesced load of
+// 64 blocks, their CRC-32 and shift tree, the W+K expansion -- and hands W+K over through LDS
+// (20 ds_write_b128 per lane); the chain wave (s_setprio 3) only copies its block's 80 words
+// into registers (20 ds_read_b128 per lane per super-step) and runs the 64 chains.  The chain
+// wave's instruction stream is then 405 + 5 per block plus ~30 per 64 blocks.
+constexpr int kPipeJobs = 4;  // jobs per workgroup (one per SIMD)
+
+struct PipeSlot {  // one job's hand-over area
+  uint4 wk[20][64];  // [word quad][lane]: lane l's block W+K[4q..4q+3] -- conflict-free b128 access
+  DeepMsg msg;       // the head's result (chain -> producer), then the final CRC (producer -> chain)
+  int started;       // chain -> producer: msg holds the head's result
+  int ready;         // producer -> chain: super-steps whose W+K has been written
+  int taken;         // chain -> producer: super-steps whose W+K the chain has copied out
+  int crc_done;      // producer -> chain: msg.crc_raw is the CRC after the bulk
+};
+
+struct PipeLDS {
+  Tables tab;                                // 36 KiB
+  PipeSlot slot[kPipeJobs];                  // 4 x 20 KiB
+  uint8_t xs[kPipeJobs][64];
+  uint8_t fin[kPipeJobs][192];
+};
+
+__device__ __forceinline__ int lds_acquire(const int* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_release(int* p, int v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+template <int kSleep>
+__device__ __forceinline__ void wait_at_least(const int* p, int v) {
+  while (lds_acquire(p) < v) __builtin_amdgcn_s_sleep(kSleep);
+}
+
+// Producer side of deep_bulk: super-steps of up to 64 blocks, right-aligned in the lanes.
+template <bool kAligned16>
+__device__ void pipe_produce(const Tables& T, PipeSlot& P, int lane, const uint8_t* q, uint64_t nbulk, bool do_sha,
+                             bool do_crc, uint32_t& crc_raw) {
+  uint32_t le[16];
+  uint64_t b0 = 0;
+  int nb = (int)(nbulk < 64 ? nbulk : 64);
+  {
+    const int bi = lane - (64 - nb);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) le[k] = 0;
+    if (bi >= 0) load_block_le<kAligned16>(EFES_RANGE(q + 64 * (uint64_t)bi, 64, q, 64 * nbulk, "pipe-bulk0"), le);
+  }
+  for (int step = 0; b0 < nbulk; ++step) {
+    if (do_crc) {
+      uint32_t r = crc_words_raw(T.slice8, 0u, le);
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        const uint32_t o = __shfl_xor(r, 1 << k);
+        const bool right = (lane >> k) & 1;
+        r = crc_shift(T.shift[k], right ? o : r) ^ (right ? r : o);
+      }
+      if (nb == 64) {
+        crc_raw = crc_shift(T.shift[6], crc_raw);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 6; ++k)
+          if ((nb >> k) & 1) crc_raw = crc_shift(T.shift[k], crc_raw);
+      }
+      crc_raw ^= r;
+    }
+    uint32_t x[80];
+    if (do_sha) {
+      uint32_t w[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) w[k] = bswap(le[k]);
+      expand_wk(w, x);
+    }
+    const uint64_t b1 = b0 + (uint64_t)nb;
+    const int nb1 = (int)((nbulk - b1) < 64 ? (nbulk - b1) : 64);
+    if (b1 < nbulk) {
+      const int bj = lane - (64 - nb1);
+#pragma unroll
+      for (int k = 0; k < 16; ++k) le[k] = 0;
+      if (bj >= 0) load_block_le<kAligned16>(EFES_RANGE(q + 64 * (b1 + (uint64_t)bj), 64, q, 64 * nbulk, "pipe-bulk1"), le);
+    }
+    if (do_sha) {
+      wait_at_least<8>(&P.taken, step);  // the chain has copied super-step step-1 out
+#pragma unroll
+      for (int k = 0; k < 20; ++k) P.wk[k][lane] = make_uint4(x[4 * k], x[4 * k + 1], x[4 * k + 2], x[4 * k + 3]);
+      lds_release(&P.ready, step + 1);
+    }
+    b0 = b1;
+    nb = nb1;
+  }
+}
+
+// Chain side: per super-step, copy this lane's block W+K out of LDS and run the nb chains.
+__device__ void pipe_consume(PipeSlot& P, int lane, uint64_t nbulk, uint32_t (&h)[5]) {
+  uint64_t b0 = 0;
+  for (int step = 0; b0 < nbulk; ++step) {
+    const int nb = (int)((nbulk - b0) < 64 ? (nbulk - b0) : 64);
+    wait_at_least<1>(&P.ready, step + 1);
+    uint32_t x[80];
+#pragma unroll
+    for (int k = 0; k < 20; ++k) {
+      const uint4 v = P.wk[k][lane];
+      x[4 * k] = v.x; x[4 * k + 1] = v.y; x[4 * k + 2] = v.z; x[4 * k + 3] = v.w;
+    }
+    lds_release(&P.taken, step + 1);  // (release: the reads above complete first)
+    uint32_t hv[5] = {h[0], h[1], h[2], h[3], h[4]}, hs[5];
+    auto block = [&]() {
+      uint32_t s[5] = {hv[0], hv[1], hv[2], hv[3], hv[4]};
+      ChainRegs<0>::run(s, x);
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {
+        hs[k] = hv[k] + s[k];                                                           // sha1.go:193-197
+        hv[k] = (uint32_t)__builtin_amdgcn_mov_dpp((int)hs[k], 0x138, 0xf, 0xf, true);  // wave_shr:1
+      }
+    };
+    const int nbu = (int)uniform32((uint32_t)nb);
+    int j = 0;
+    for (; j + 2 <= nbu; j += 2) { block(); block(); }
+    if (j < nbu) block();
+#pragma unroll
+    for (int k = 0; k < 5; ++k) h[k] = (uint32_t)__builtin_amdgcn_readlane((int)hs[k], 63);
+    b0 += (uint64_t)nb;
+  }
+}
+
+__global__ __launch_bounds__(128 * kPipeJobs, 1) void deep_kernel(const efes_job* __restrict__ jobs, uint32_t njobs,
                                                                   const Tables* __restrict__ tabs) {
-  __shared__ __attribute__((aligned(16))) DeepLDS L;
+  __shared__ __attribute__((aligned(16))) PipeLDS L;
   {
     const uint4* src = reinterpret_cast<const uint4*>(tabs);
     uint4* dst = reinterpret_cast<uint4*>(&L.tab);
     for (int i = threadIdx.x; i < (int)(sizeof(Tables) / 16); i += blockDim.x) dst[i] = src[i];
+    if (threadIdx.x < kPipeJobs) {
+      PipeSlot& P = L.slot[threadIdx.x];
+      P.started = P.ready = P.taken = P.crc_done = 0;
+    }
   }
   __syncthreads();
   const int wave = (int)uniform32(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  const uint32_t j = blockIdx.x * kDeepWaves + (uint32_t)wave;
+  const int w = wave & (kPipeJobs - 1);
+  const uint32_t j = blockIdx.x * kPipeJobs + (uint32_t)w;
   if (j >= njobs) return;
+  PipeSlot& P = L.slot[w];
   const DeepJob J = load_job(jobs, j, lane);
-  uint8_t* xs = L.xs[wave][0];
-  const DeepMsg M = deep_head(L, lane, J, xs);
-  if (M.live) deep_rest(L, lane, J, xs, L.fin[wave], M);
+  const bool do_sha = J.st != nullptr, do_crc = J.cs != nullptr;
+  if (wave < kPipeJobs) {  // ---- chain wave
+    __builtin_amdgcn_s_setprio(3);
+    DeepMsg M = deep_head(L.tab, lane, J, L.xs[w]);
+    if (lane == 0) P.msg = M;
+    lds_release(&P.started, 1);
+    if (!M.live) return;
+    if (do_sha) pipe_consume(P, lane, M.nbulk, M.h);
+    wait_at_least<1>(&P.crc_done, 1);
+    M.crc_raw = uniform32(P.msg.crc_raw);
+    M.done = M.nbulk;
+    deep_rest(L.tab, lane, J, L.xs[w], L.fin[w], M);
+  } else {  // ---- producer wave
+    wait_at_least<4>(&P.started, 1);
+    const DeepMsg M = uniform_msg(P.msg);
+    if (!M.live) return;
+    uint32_t crc_raw = M.crc_raw;
+    if (M.nbulk) {
+      if ((reinterpret_cast<uintptr_t>(M.q) & 15) == 0)
+        pipe_produce<true>(L.tab, P, lane, M.q, M.nbulk, do_sha, do_crc, crc_raw);
+      else
+        pipe_produce<false>(L.tab, P, lane, M.q, M.nbulk, do_sha, do_crc, crc_raw);
+    }
+    if (lane == 0) P.msg.crc_raw = crc_raw;
+    lds_release(&P.crc_done, 1);
+  }
 }
 
 // ================================================================== grouped DEEP kernel
@@ -449,7 +623,7 @@ __global__ __launch_bounds__(64 * kDeepWaves, 1) void deep_kernel(const efes_job
 // (left-over bulk blocks through deep_bulk, tail, Sum, write-back).  Jobs are expected
 // longest-first (efes_plan_batch) so the jobs of a wave have similar lengths.
 template <int G, bool kAligned16>
-__device__ void group_bulk(DeepLDS& L, int lane, DeepMsg* msgs, uint64_t S, bool any_sha, bool any_crc) {
+__device__ void group_bulk(const Tables& T, int lane, DeepMsg* msgs, uint64_t S, bool any_sha, bool any_crc) {
   constexpr int kLG = G == 4 ? 2 : G == 8 ? 3 : G == 16 ? 4 : 5;
   static_assert((1 << kLG) == G, "G must be 4, 8, 16 or 32");
   const int m = lane / G, i = lane % G;
@@ -464,14 +638,14 @@ __device__ void group_bulk(DeepLDS& L, int lane, DeepMsg* msgs, uint64_t S, bool
   if (live) load_block_le<kAligned16>(q + 64 * (uint64_t)i, le);
   for (uint64_t st = 0; st < S; ++st) {
     if (any_crc) {
-      uint32_t r = crc_words_raw(L.tab.slice8, 0u, le);
+      uint32_t r = crc_words_raw(T.slice8, 0u, le);
 #pragma unroll
       for (int k = 0; k < kLG; ++k) {  // crc(A||B) = shift(crc(A), |B|) ^ crc(B) within the job's G lanes
         const uint32_t o = __shfl_xor(r, 1 << k);
         const bool right = (lane >> k) & 1;
-        r = crc_shift(L.tab.shift[k], right ? o : r) ^ (right ? r : o);
+        r = crc_shift(T.shift[k], right ? o : r) ^ (right ? r : o);
       }
-      crc_raw = crc_shift(L.tab.shift[kLG], crc_raw) ^ r;  // running crc advanced over G*64 bytes
+      crc_raw = crc_shift(T.shift[kLG], crc_raw) ^ r;  // running crc advanced over G*64 bytes
     }
     uint32_t x[80];
     if (any_sha) {
@@ -513,21 +687,6 @@ __device__ void group_bulk(DeepLDS& L, int lane, DeepMsg* msgs, uint64_t S, bool
   wave_lds_sync();
 }
 
-// DeepMsg field read back from LDS as a wave-uniform value.
-__device__ __forceinline__ DeepMsg uniform_msg(const DeepMsg& s) {
-  DeepMsg M;
-#pragma unroll
-  for (int k = 0; k < 5; ++k) M.h[k] = uniform32(s.h[k]);
-  M.crc_raw = uniform32(s.crc_raw);
-  M.q = reinterpret_cast<const uint8_t*>(uniform64(reinterpret_cast<uint64_t>(s.q)));
-  M.pos = uniform64(s.pos);
-  M.nbulk = uniform64(s.nbulk);
-  M.done = uniform64(s.done);
-  M.nx_new = (int64_t)uniform64((uint64_t)s.nx_new);
-  M.live = uniform32(s.live);
-  M.joint = uniform32(s.joint);
-  return M;
-}
 
 template <int G>
 __global__ __launch_bounds__(64 * kDeepWaves, 1) void group_kernel(const efes_job* __restrict__ jobs, uint32_t njobs,
@@ -551,7 +710,7 @@ __global__ __launch_bounds__(64 * kDeepWaves, 1) void group_kernel(const efes_jo
   for (int m = 0; m < kJobs; ++m) {
     const uint32_t j = j0 + (uint32_t)m;
     DeepMsg M{};
-    if (j < njobs) M = deep_head(L, lane, load_job(jobs, j, lane), L.xs[wave][m]);
+    if (j < njobs) M = deep_head(L.tab, lane, load_job(jobs, j, lane), L.xs[wave][m]);
     wave_lds_sync();
     if (lane == 0) msgs[m] = M;
   }
@@ -582,8 +741,8 @@ __global__ __launch_bounds__(64 * kDeepWaves, 1) void group_kernel(const efes_jo
       if (lane == 0) msgs[m].joint = M.live && (M.nbulk - M.done) / G > 0 ? 1u : 0u;
     }
     wave_lds_sync();
-    if (all16) group_bulk<G, true>(L, lane, msgs, S, any_sha, any_crc);
-    else group_bulk<G, false>(L, lane, msgs, S, any_sha, any_crc);
+    if (all16) group_bulk<G, true>(L.tab, lane, msgs, S, any_sha, any_crc);
+    else group_bulk<G, false>(L.tab, lane, msgs, S, any_sha, any_crc);
   }
 
   // ---- per job: left-over blocks, tail, Sum, write-back
@@ -593,7 +752,7 @@ __global__ __launch_bounds__(64 * kDeepWaves, 1) void group_kernel(const efes_jo
     const DeepMsg M = uniform_msg(msgs[m]);
     if (!M.live) continue;
     const DeepJob J = load_job(jobs, j, lane);
-    deep_rest(L, lane, J, L.xs[wave][m], L.fin[wave], M);
+    deep_rest(L.tab, lane, J, L.xs[wave][m], L.fin[wave], M);
   }
 }
 
@@ -883,8 +1042,8 @@ __global__ void fill_kernel(uint64_t* __restrict__ dst, uint64_t nwords, uint64_
 // ================================================================== launchers
 hipError_t launch_deep(const efes_job* jobs, uint32_t njobs, const Tables* tabs, hipStream_t s) {
   if (njobs == 0) return hipSuccess;
-  const uint32_t grid = (njobs + kDeepWaves - 1) / kDeepWaves;
-  hipLaunchKernelGGL(deep_kernel, dim3(grid), dim3(64 * kDeepWaves), 0, s, jobs, njobs, tabs);
+  const uint32_t grid = (njobs + kPipeJobs - 1) / kPipeJobs;
+  hipLaunchKernelGGL(deep_kernel, dim3(grid), dim3(128 * kPipeJobs), 0, s, jobs, njobs, tabs);
   return hipGetLastError();
 }
 
@@ -917,7 +1076,8 @@ hipError_t launch_group(const efes_job* jobs, uint32_t njobs, int G, const Table
     case 8: return launch_reserving(group_kernel<8>, grid, block, exclusive, s, jobs, njobs, tabs);
     case 16: return launch_reserving(group_kernel<16>, grid, block, exclusive, s, jobs, njobs, tabs);
     case 32: return launch_reserving(group_kernel<32>, grid, block, exclusive, s, jobs, njobs, tabs);
-    case 64: return launch_reserving(deep_kernel, grid, block, exclusive, s, jobs, njobs, tabs);
+    case 64: return launch_reserving(deep_kernel, dim3((njobs + kPipeJobs - 1) / kPipeJobs), dim3(128 * kPipeJobs),
+                                     exclusive, s, jobs, njobs, tabs);
     default: return hipErrorInvalidValue;
   }
 }

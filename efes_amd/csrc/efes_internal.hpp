@@ -35,7 +35,10 @@ efes_queue* stream_queue(efes_ctx* ctx, int* rc);
 
 // Launchers (host side, defined in efes_kernels.hip).
 hipError_t launch_deep(const efes_job* jobs, uint32_t njobs, const Tables* tabs, hipStream_t s);
-hipError_t launch_wide(const efes_job* jobs, uint32_t njobs, const Tables* tabs, hipStream_t s);
+// exclusive: one workgroup (one wave per SIMD) per CU, so a long job's lane is never slowed by
+// other waves on its SIMD.
+hipError_t launch_wide(const efes_job* jobs, uint32_t njobs, const Tables* tabs, hipStream_t s,
+                       bool exclusive = false);
 // Grouped DEEP: 64/G jobs per wave, G in {4, 8, 16, 32} (64 = launch_deep).  exclusive: each
 // workgroup reserves all LDS of its CU, so no other workgroup shares the CU's SIMDs.
 hipError_t launch_group(const efes_job* jobs, uint32_t njobs, int G, const Tables* tabs, hipStream_t s,

@@ -1082,11 +1082,10 @@ hipError_t launch_group(const efes_job* jobs, uint32_t njobs, int G, const Table
   }
 }
 
-hipError_t launch_wide(const efes_job* jobs, uint32_t njobs, const Tables* tabs, hipStream_t s) {
+hipError_t launch_wide(const efes_job* jobs, uint32_t njobs, const Tables* tabs, hipStream_t s, bool exclusive) {
   if (njobs == 0) return hipSuccess;
   const uint32_t per = 64 * kWideWaves;
-  hipLaunchKernelGGL(wide_kernel, dim3((njobs + per - 1) / per), dim3(per), 0, s, jobs, njobs, tabs);
-  return hipGetLastError();
+  return launch_reserving(wide_kernel, dim3((njobs + per - 1) / per), dim3(per), exclusive, s, jobs, njobs, tabs);
 }
 
 hipError_t launch_fill(void* dst, size_t bytes, uint64_t seed, hipStream_t s) {

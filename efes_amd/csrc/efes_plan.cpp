@@ -189,7 +189,7 @@ int efes_plan_batch(efes_ctx* ctx, const uint64_t* lengths, uint32_t n, uint32_t
       c += x;
       c += *c == ',';
       const uint32_t take = (uint32_t)std::min<unsigned long long>(d, n - used);
-      if (take) fp[fn++] = efes_plan_part{take, mode_of(g), (x && g != kWideLanes) ? 1u : 0u, 0u};
+      if (take) fp[fn++] = efes_plan_part{take, mode_of(g), x ? 1u : 0u, 0u};
       used += take;
     }
     if (ok && used < n) {
@@ -220,7 +220,7 @@ int efes_hash_submit_plan(efes_ctx* ctx, const efes_job* jobs, const efes_plan* 
   efes::DeviceGuard guard(ctx->device);
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
   auto launch = [&](const efes_plan_part& p, const efes_job* first, hipStream_t st) {
-    if (p.mode == EFES_MODE_WIDE) return efes::launch_wide(first, p.jobs, ctx->d_tabs, st);
+    if (p.mode == EFES_MODE_WIDE) return efes::launch_wide(first, p.jobs, ctx->d_tabs, st, p.exclusive != 0);
     return efes::launch_group(first, p.jobs, lanes_of(p.mode), ctx->d_tabs, st, p.exclusive != 0);
   };
   std::lock_guard<std::mutex> lk(ctx->plan_mu);

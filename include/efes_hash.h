@@ -136,7 +136,7 @@ int efes_auto_mode(const efes_ctx* ctx, uint32_t njobs);
 typedef struct efes_plan_part {
     uint32_t jobs;       /* consecutive jobs of this part (in plan order) */
     int32_t mode;        /* EFES_MODE_DEEP, EFES_MODE_GROUPn or EFES_MODE_WIDE */
-    uint32_t exclusive;  /* 1: workgroups reserve their CU (DEEP/GROUPn only) */
+    uint32_t exclusive;  /* 1: each workgroup reserves its CU (one wave per SIMD) */
     uint32_t _reserved;
 } efes_plan_part;
 typedef struct efes_plan {

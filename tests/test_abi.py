@@ -146,3 +146,33 @@ def test_integration_doc_binds_only_declared_symbols():
     assert not missing, missing
     for const in set(re.findall(r"\bC\.(EFES_\w+)", doc)):
         assert re.search(r"#define\s+%s\b" % const, open(HEADER).read()), const
+
+
+def test_plan_struct_layout_matches_header(tmp_path, efes_lib):
+    """efes_plan / efes_plan_part (the batch planner's C structs) == the ctypes mirror."""
+    prog = tmp_path / "plan.c"
+    prog.write_text("""
+#include <stdio.h>
+#include <stddef.h>
+#include "efes_hash.h"
+int main(void) {
+  printf("%zu %zu %zu %zu %zu %zu %d\\n", sizeof(efes_plan_part), offsetof(efes_plan_part, exclusive),
+         sizeof(efes_plan), offsetof(efes_plan, nparts), offsetof(efes_plan, part), offsetof(efes_plan, est_seconds),
+         EFES_PLAN_MAX_PARTS);
+  return 0;
+}""")
+    exe = tmp_path / "plan"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.dirname(HEADER), str(prog), "-o", str(exe)], check=True)
+    got = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()
+    P, Q = efes_lib.Plan, efes_lib.PlanPart
+    assert got == [str(v) for v in (ctypes.sizeof(Q), Q.exclusive.offset, ctypes.sizeof(P), P.nparts.offset,
+                                    P.part.offset, P.est_seconds.offset, efes_lib.PLAN_MAX_PARTS)]
+
+
+def test_auto_mode_by_job_count(efes_lib):
+    """efes_auto_mode (ctx NULL = one MI355X, 1024 SIMDs): DEEP, GROUP32..GROUP4, then WIDE."""
+    L = efes_lib.lib()
+    G = efes_lib.MODE_GROUP
+    want = {1: efes_lib.MODE_DEEP, 1024: efes_lib.MODE_DEEP, 1025: G[32], 2048: G[32], 4096: G[16], 8192: G[8],
+            8193: G[4], 24576: G[4], 24577: efes_lib.MODE_WIDE, 131072: efes_lib.MODE_WIDE}
+    assert {n: L.efes_auto_mode(None, n) for n in want} == want

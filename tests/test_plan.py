@@ -73,7 +73,7 @@ def test_empty_and_zero_lengths():
     ("64:5000", [(3000, MODE_DEEP, False)]),
     ("4:10x,16:20", [(10, MODE_GROUP[4], True), (20, MODE_GROUP[16], False), (2970, MODE_WIDE, False)]),
     ("0:3000", [(3000, MODE_WIDE, False)]),
-    ("0:5x", [(5, MODE_WIDE, False), (2995, MODE_WIDE, False)]),
+    ("0:5x", [(5, MODE_WIDE, True), (2995, MODE_WIDE, False)]),
 ])
 def test_force_override(monkeypatch, force, expect):
     monkeypatch.setenv("EFES_PLAN_FORCE", force)

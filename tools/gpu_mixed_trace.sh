@@ -15,7 +15,7 @@ path = glob.glob(f"gpurun_out/mixtrace/{tag}/**/run_kernel_trace.csv", recursive
 rows = [r for r in csv.DictReader(open(path)) if "efes::" in r["Kernel_Name"] and "fill" not in r["Kernel_Name"]]
 t0 = min(int(r["Start_Timestamp"]) for r in rows)
 for r in rows:
-    print(tag, r["Kernel_Name"].split("(")[0], "grid", r["Grid_Size"], "lds", r["LDS_Block_Size"],
+    print(tag, r["Kernel_Name"].split("(")[0], "grid", r.get("Grid_Size_X"), "lds", r["LDS_Block_Size"],
           "start %.3f end %.3f s" % ((int(r["Start_Timestamp"]) - t0) / 1e9, (int(r["End_Timestamp"]) - t0) / 1e9))
 PY
 done

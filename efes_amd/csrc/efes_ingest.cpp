@@ -103,7 +103,7 @@ int efes_host_free(efes_ctx* ctx, void* p) {
 }
 
 // EFES_HOST_ZERO_COPY: the data is pinned, device-mapped host memory (efes_host_alloc); one DEEP
-// launch reads it in place over PCIe (coalesced 4 KiB per wave, prefetched a super-step ahead
+// (or grouped-DEEP, efes::pcie_mode) launch reads it in place over PCIe (coalesced 4 KiB per wave, prefetched a super-step ahead
 // of the chain) -- no staging, no segments.
 static int hash_host_mapped(efes_ctx* ctx, const efes_job* jobs, uint32_t n, efes_host_stats* stats) {
   std::vector<efes_job> hj(jobs, jobs + n);
@@ -143,7 +143,7 @@ static int hash_host_mapped(efes_ctx* ctx, const efes_job* jobs, uint32_t n, efe
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) return EFES_ERR_HIP;
   const auto t0 = std::chrono::steady_clock::now();
-  int rc = efes_hash_submit_mode(ctx, d_jobs.as<efes_job>(), n, s, EFES_MODE_DEEP);
+  int rc = efes_hash_submit_mode(ctx, d_jobs.as<efes_job>(), n, s, efes::pcie_mode(ctx, n));
   if (rc) return rc;
   e = hipMemcpyAsync(hs.data(), d_states.p, sizeof(efes_sha1_state) * n, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipMemcpyAsync(hc.data(), d_crcs.p, sizeof(efes_crc32_state) * n, hipMemcpyDeviceToHost, s);

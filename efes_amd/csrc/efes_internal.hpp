@@ -45,6 +45,14 @@ hipError_t launch_group(const efes_job* jobs, uint32_t njobs, int G, const Table
                         bool exclusive = false);
 hipError_t launch_fill(void* dst, size_t bytes, uint64_t seed, hipStream_t s);
 
+// Kernel shape for jobs whose bytes are read over PCIe in place (pinned, device-mapped host
+// memory): AUTO's choice, but never WIDE (its scattered 64-B lane reads are slow over PCIe;
+// DEEP/GROUPn read G*64 contiguous bytes per job).
+inline int pcie_mode(const efes_ctx* ctx, uint32_t njobs) {
+  const int m = efes_auto_mode(ctx, njobs);
+  return m == EFES_MODE_WIDE ? EFES_MODE_GROUP4 : m;
+}
+
 // Lanes per job of a grouped-DEEP mode (EFES_MODE_GROUPn -> n), 0 for other modes.
 inline int group_of_mode(int mode) {
   switch (mode) {

@@ -70,6 +70,8 @@ def parse_args(argv=None):
     p.add_argument("--segment-bytes", type=int, default=1 << 20, help="host-inclusive pipeline segment")
     p.add_argument("--ingest-leg", choices=["auto", "on", "off"], default="auto",
                    help="also report BASELINE configs[4] per-GPU (auto = N=1 only)")
+    p.add_argument("--mixed-leg", choices=["auto", "on", "off"], default="auto",
+                   help="also report BASELINE configs[3] (planned mixed-size batch); auto = N=1 only")
     p.add_argument("--dist-backend", default="nccl", help="N>1 timing barrier/max only (no data-path collective)")
     p.add_argument("--all-ranks-on-device0", action="store_true",
                    help="rehearse the N>1 path on a 1-GPU box (use with --dist-backend gloo)")
@@ -357,6 +359,38 @@ def ingest_leg(args, rank: int, world: int, ctx, device: str, stream, mode: int)
             "note": "many concurrent chunks per GPU (configs[4] per-GPU queue); not `value`"}
 
 
+def mixed_leg(args, rank: int, world: int, ctx, device: str, stream):
+    """BASELINE configs[3] beside the metric: 65 536 chunks of the eleven ChunkSize values
+    64K..64M (752 GiB, aliasing a 64 GiB pool), placed by efes_plan_batch (grouped-DEEP parts
+    on CUs of their own, concurrent with WIDE); one warm-up and one timed step."""
+    import argparse as _ap
+
+    import torch
+
+    from efes_amd._lib import MODE_DEEP, MODE_GROUP, MODE_WIDE
+    from efes_amd.batch import MODE_PLAN
+
+    a = _ap.Namespace(**vars(args))
+    a.workload = "mixed"
+    with torch.cuda.stream(stream):
+        data, batches, step_bytes, config = make_workload(a, rank, world, ctx, device, stream)
+        for b in batches:
+            b.make_plan()
+        wall, kernel_ms = run_timed(batches, len(batches), 1, MODE_PLAN, device, stream, None)
+    total = sum(step_bytes)
+    names = {MODE_DEEP: "deep_kernel", MODE_WIDE: "wide_kernel"}
+    names.update({v: f"group_kernel<{g}>" for g, v in MODE_GROUP.items()})
+    parts = [{"jobs": j, "kernel": names[m], "exclusive_cus": x} for j, m, x in batches[0].plan.parts()]
+    achieved = total / len(batches) / (kernel_ms * 1e-3) / 1e9
+    del data, batches
+    torch.cuda.empty_cache()
+    return {"value": round(total / wall / GiB, 3), "unit": "GiB/s", "workload": config["workload"],
+            "chunks": config["chunks_per_gpu"], "bytes": total, "plan": parts,
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBPS, 5), "kernel_ms": round(kernel_ms, 3)},
+            "note": "makespan set by the 64 MiB chunks' SHA-1 chains (DESIGN.md §4 batch planner); not `value`"}
+
+
 def main(argv=None):
     args = parse_args(argv)
     import torch
@@ -463,6 +497,8 @@ def main(argv=None):
                                                    batches[0])
         if args.ingest_leg == "on" or (args.ingest_leg == "auto" and world == 1):
             out["ingest_config"] = ingest_leg(args, rank, world, ctx, device, stream, MODE_AUTO)
+        if args.mixed_leg == "on" or (args.mixed_leg == "auto" and world == 1):
+            out["mixed_config"] = mixed_leg(args, rank, world, ctx, device, stream)
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             threads = args.cpu_threads or host_threads()
             out["cpu_baseline"] = cpu_baseline(batches[0], data, min(n, args.cpu_max_chunks), chunk, threads,

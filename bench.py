@@ -67,7 +67,7 @@ def parse_args(argv=None):
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--host-inclusive", choices=["auto", "on", "off"], default="auto",
                    help="also time the host-resident path (pinned H2D + hash); auto = N=1 only")
-    p.add_argument("--segment-bytes", type=int, default=1 << 20, help="host-inclusive pipeline segment")
+    p.add_argument("--segment-bytes", type=int, default=256 << 10, help="host-inclusive pipeline segment")
     p.add_argument("--ingest-leg", choices=["auto", "on", "off"], default="auto",
                    help="also report BASELINE configs[4] per-GPU (auto = N=1 only)")
     p.add_argument("--mixed-leg", choices=["auto", "on", "off"], default="auto",

@@ -177,7 +177,9 @@ int efes_hash_host(efes_ctx* ctx, const efes_job* jobs, uint32_t n, uint64_t seg
     DeviceGuard g(ctx->device);
     return hash_host_mapped(ctx, jobs, n, stats);
   }
-  const uint64_t seg = segment_bytes ? (segment_bytes + 63) & ~uint64_t(63) : (uint64_t)1 << 20;
+  // 256 KiB: short segments keep the hash of the last one (the exposed tail) small; measured
+  // 50.8 GiB/s against 45.4 at 1 MiB for 1024 x 4 MiB (H2D ceiling 57.6 GB/s, mb_h2d.hip).
+  const uint64_t seg = segment_bytes ? (segment_bytes + 63) & ~uint64_t(63) : (uint64_t)256 << 10;
   uint64_t nseg = 1;
   for (uint32_t i = 0; i < n; ++i) nseg = std::max<uint64_t>(nseg, (jobs[i].length + seg - 1) / seg);
 

@@ -162,7 +162,7 @@ int efes_fill_synthetic(efes_ctx* ctx, void* dst_device, size_t bytes, uint64_t 
 /* ---- host-resident ingest -------------------------------------------------------------
  * The reference's path starts in host memory (a socket buffer, filereceiver.go:208-209).
  * efes_hash_host runs the jobs of a HOST array whose data/sha1/crc32/sum/status pointers are
- * all HOST memory: segment s (segment_bytes, rounded up to 64; 0 = 1 MiB) of every message is
+ * all HOST memory: segment s (segment_bytes, rounded up to 64; 0 = 256 KiB) of every message is
  * copied H2D with hipMemcpyAsync on a copy stream into one of two device slots while segment
  * s-1 is hashed on the context stream; states stay on the device between segments (the
  * per-PATCH resume of filereceiver.go:182-226); states, sums and status are copied back at

@@ -160,7 +160,9 @@ struct DeepJob {
   uint32_t flags;
 };
 
-// Bulk blocks q[0 .. 64*nbulk).  Per super-step of up to 64 blocks (4 KiB, one coalesced
+// Bulk blocks q[0 .. 64*nbulk) of one job by one wave alone (the one-job path, used for a
+// grouped wave's left-over blocks through deep_rest).  The DEEP kernel proper splits this same super-step between a producer and a chain wave
+// (pipe_produce / pipe_consume below).  Per super-step of up to 64 blocks (4 KiB, one coalesced
 // load per lane, prefetched a super-step ahead): lane off+i holds block i, computes its raw
 // CRC-32 (slicing-by-8, LDS tables) and expands its schedule W[t]+K[t] into its own 80 VGPRs.
 // The block CRCs are merged by a 6-level GF(2) shift tree.  Then the wave runs the SHA-1

@@ -1,7 +1,7 @@
 """Developer tool: run the golden synthetic vectors through the range-checked debug build.
 
 Build:  hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -DEFES_CHECKED -I include \
-            -o efes_amd/lib/libefeshash_checked.so efes_amd/csrc/efes_kernels.hip efes_amd/csrc/efes_api.cpp
+            -o efes_amd/lib/libefeshash_checked.so efes_amd/csrc/efes_*.hip efes_amd/csrc/efes_*.cpp
 Run:    EFES_LIB_OVERRIDE=$PWD/efes_amd/lib/libefeshash_checked.so python tools/debug_checked.py
 """
 import json

@@ -789,3 +789,24 @@ def test_planned_batch_forced_parts(env, oracle, force, monkeypatch):
     for i in range(n):
         dat = host[int(offsets[i]):int(offsets[i]) + int(lengths[i])].tobytes()
         assert shas[i] == hashlib.sha1(dat).hexdigest() and crcs[i] == zlib.crc32(dat), (force, i)
+
+
+def test_planned_batch_random_lengths(env, oracle):
+    """The planner's own plan (no forcing) on a heavy-tailed length mix: every digest correct."""
+    from efes_amd.batch import MODE_PLAN
+    rng = np.random.default_rng(31)
+    n = 3000
+    lengths = np.minimum(rng.lognormal(10.0, 2.0, n).astype(np.int64), 6 << 20)
+    lengths[rng.integers(0, n, 40)] = 0
+    offsets = np.concatenate([[0], np.cumsum(lengths + 17)[:-1]]).astype(np.uint64)
+    host = oracle.fill_synthetic(int((lengths + 17).sum()) + 64, 2024)
+    buf = device_buffer(env, host)
+    b = env["DeviceBatch"](buf.data_ptr(), offsets, lengths, fresh=True, ctx=env["ctx"])
+    b.make_plan()
+    assert sum(p[0] for p in b.plan.parts()) == n
+    b.run(MODE_PLAN)
+    assert (b.status_host() == 0).all()
+    shas, crcs = b.sha1_hex(), b.crc_sum()
+    for i in range(n):
+        d = host[int(offsets[i]):int(offsets[i]) + int(lengths[i])].tobytes()
+        assert shas[i] == hashlib.sha1(d).hexdigest() and crcs[i] == zlib.crc32(d), (i, int(lengths[i]))

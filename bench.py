@@ -60,7 +60,8 @@ def parse_args(argv=None):
                    help="synchronize after every step and print progress to stderr (long workloads)")
     p.add_argument("--ingest-tib", type=float, default=10.0)
     p.add_argument("--ingest-scale", type=float, default=1.0)
-    p.add_argument("--ingest-batch", type=int, default=65536)
+    p.add_argument("--ingest-batch", type=int, default=196608,
+                   help="chunks per launch: 3 WIDE waves per SIMD (134 VGPRs -> 3 resident) x 1024 SIMDs x 64")
     p.add_argument("--sha1-only", action="store_true", help="BASELINE configs[1] (no CRC-32)")
     p.add_argument("--cpu-threads", type=int, default=0, help="cpu_baseline threads (0 = host share, max 16)")
     p.add_argument("--cpu-max-chunks", type=int, default=1024)
@@ -341,7 +342,10 @@ def ingest_leg(args, rank: int, world: int, ctx, device: str, stream, mode: int)
     import torch
 
     a = _ap.Namespace(**vars(args))
-    a.workload, a.ingest_batch, a.ingest_scale = "ingest", 131072, args.ingest_scale
+    # launches of 196 608 chunks = 3 resident WIDE waves on every SIMD (then the remainder):
+    # 2 613-2 673 GiB/s against 2 395-2 443 for launches of 131 072 (2 waves per SIMD) and 2 408 for one
+    # launch of all 327 680 (profiles/r01_sweeps/ingest_batch_*.json)
+    a.workload, a.ingest_batch, a.ingest_scale = "ingest", 196608, args.ingest_scale
     with torch.cuda.stream(stream):
         data, batches, step_bytes, config = make_workload(a, rank, world, ctx, device, stream)
         wall, kernel_ms = run_timed(batches, len(batches), 1, mode, device, stream, None)

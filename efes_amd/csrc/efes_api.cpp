@@ -127,6 +127,15 @@ void efes::build_tables(Tables* t) {
   }
 }
 
+void efes::build_pos_tables(const Tables* t, PosTables* out) {
+  for (int p = 0; p < 64; ++p)
+    for (uint32_t b = 0; b < 256; ++b) {
+      uint32_t crc = 0;  // raw register, crc32.go:125 per byte
+      for (int i = 0; i < 64; ++i) crc = t->slice8[0][(crc ^ (i == p ? b : 0u)) & 0xff] ^ (crc >> 8);
+      out->pos[p][b] = crc;
+    }
+}
+
 // ======================================================================= C ABI
 extern "C" {
 
@@ -165,9 +174,12 @@ int efes_ctx_create(int device, efes_ctx** out) {
   if (!ctx) return EFES_ERR_NOMEM;
   ctx->device = device;
   DeviceGuard g(device);
-  Tables* host = static_cast<Tables*>(malloc(sizeof(Tables)));
+  // Tables followed by PosTables in one allocation (efes_internal.hpp)
+  const size_t tab_bytes = sizeof(Tables) + sizeof(efes::PosTables);
+  Tables* host = static_cast<Tables*>(malloc(tab_bytes));
   if (!host) { delete ctx; return EFES_ERR_NOMEM; }
   efes::build_tables(host);
+  efes::build_pos_tables(host, reinterpret_cast<efes::PosTables*>(host + 1));
   ctx->cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
   hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming);
@@ -175,8 +187,8 @@ int efes_ctx_create(int device, efes_ctx** out) {
     e = hipStreamCreateWithFlags(&ctx->side[i], hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_join[i], hipEventDisableTiming);
   }
-  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&ctx->d_tabs), sizeof(Tables));
-  if (e == hipSuccess) e = hipMemcpy(ctx->d_tabs, host, sizeof(Tables), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&ctx->d_tabs), tab_bytes);
+  if (e == hipSuccess) e = hipMemcpy(ctx->d_tabs, host, tab_bytes, hipMemcpyHostToDevice);
   free(host);
   if (e != hipSuccess) {
     efes_ctx_destroy(ctx);

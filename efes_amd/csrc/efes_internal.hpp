@@ -23,6 +23,16 @@ struct Tables {
 
 void build_tables(Tables* t);  // host
 
+// Position tables for the grouped kernels' block CRC: pos[p][b] = raw CRC register (from 0)
+// after a 64-byte block whose only nonzero byte is b at position p.  The register map is
+// GF(2)-linear, so a block's raw CRC is the XOR of its 64 bytes' entries -- 64 independent LDS
+// lookups instead of slicing-by-8's chain of 8 dependent steps.  On the device the context's
+// allocation holds Tables immediately followed by PosTables (64 KiB).
+struct PosTables {
+  uint32_t pos[64][256];
+};
+void build_pos_tables(const Tables* t, PosTables* p);  // host
+
 // Go's sha1digest.Write bookkeeping of x/nx/len (sha1.go:58-79) without the compressions:
 // the host replays it so exported states carry Go's exact tail bytes (efes_api.cpp).
 int replay_write(efes_sha1_state* s, const uint8_t* p, size_t n);

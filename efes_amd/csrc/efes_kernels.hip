@@ -20,6 +20,7 @@
 //   WIDE: one lane per job (64 jobs per wave), schedule inline, CRC fused per lane.
 //         Throughput shape for many concurrent jobs.
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -145,10 +146,12 @@ struct DeepMsg {
 
 struct DeepLDS {
   Tables tab;                                    // 36 KiB
+  PosTables pos;                                 // 64 KiB, follows tab (same order as in HBM)
   uint8_t xs[kDeepWaves][kGroupMaxJobs][64];     // each job's tail buffer x (sha1.go:31)
   uint8_t fin[kDeepWaves][192];                  // padding assembly for checkSum
   DeepMsg msg[kDeepWaves][kGroupMaxJobs];
 };
+static_assert(offsetof(DeepLDS, pos) == sizeof(Tables), "DeepLDS copies Tables+PosTables in one sweep");
 
 struct DeepJob {
   const uint8_t* p;
@@ -624,8 +627,24 @@ __global__ __launch_bounds__(128 * kPipeJobs, 1) void deep_kernel(const efes_job
 // which the jobs with >= G bulk blocks left advance together; then, per job, the rest
 // (left-over bulk blocks through deep_bulk, tail, Sum, write-back).  Jobs are expected
 // longest-first (efes_plan_batch) so the jobs of a wave have similar lengths.
-template <int G, bool kAligned16>
-__device__ void group_bulk(const Tables& T, int lane, DeepMsg* msgs, uint64_t S, bool any_sha, bool any_crc) {
+// Raw CRC (register 0) of one 64-byte block: the XOR of 64 independent position-table lookups
+// (PosTables), in four accumulation chains.
+__device__ __forceinline__ uint32_t crc_block_pos(const uint32_t (&pos)[64][256], const uint32_t (&le)[16]) {
+  uint32_t acc[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int w = 0; w < 16; ++w) {
+    const uint32_t v = le[w];
+    const uint32_t x = __builtin_amdgcn_bitop3_b32(pos[4 * w][v & 0xffu], pos[4 * w + 1][(v >> 8) & 0xffu],
+                                                   pos[4 * w + 2][(v >> 16) & 0xffu], 0x96);
+    acc[w & 3] = __builtin_amdgcn_bitop3_b32(acc[w & 3], x, pos[4 * w + 3][v >> 24], 0x96);
+  }
+  return __builtin_amdgcn_bitop3_b32(acc[0], acc[1], acc[2], 0x96) ^ acc[3];
+}
+
+// kSha / kCrc are wave-uniform (any joining job needs the hash): with both, the CRC lookups and
+// the schedule expansion share one basic block, so the lookups' latency hides behind VALU work.
+template <int G, bool kAligned16, bool kSha, bool kCrc>
+__device__ void group_bulk(const Tables& T, const PosTables& P, int lane, DeepMsg* msgs, uint64_t S) {
   constexpr int kLG = G == 4 ? 2 : G == 8 ? 3 : G == 16 ? 4 : 5;
   static_assert((1 << kLG) == G, "G must be 4, 8, 16 or 32");
   const int m = lane / G, i = lane % G;
@@ -639,8 +658,8 @@ __device__ void group_bulk(const Tables& T, int lane, DeepMsg* msgs, uint64_t S,
   for (int k = 0; k < 16; ++k) le[k] = 0;
   if (live) load_block_le<kAligned16>(q + 64 * (uint64_t)i, le);
   for (uint64_t st = 0; st < S; ++st) {
-    if (any_crc) {
-      uint32_t r = crc_words_raw(T.slice8, 0u, le);
+    if constexpr (kCrc) {
+      uint32_t r = crc_block_pos(P.pos, le);  // raw CRC of this lane's block, register 0
 #pragma unroll
       for (int k = 0; k < kLG; ++k) {  // crc(A||B) = shift(crc(A), |B|) ^ crc(B) within the job's G lanes
         const uint32_t o = __shfl_xor(r, 1 << k);
@@ -650,7 +669,7 @@ __device__ void group_bulk(const Tables& T, int lane, DeepMsg* msgs, uint64_t S,
       crc_raw = crc_shift(T.shift[kLG], crc_raw) ^ r;  // running crc advanced over G*64 bytes
     }
     uint32_t x[80];
-    if (any_sha) {
+    if constexpr (kSha) {
       uint32_t w[16];
 #pragma unroll
       for (int k = 0; k < 16; ++k) w[k] = bswap(le[k]);
@@ -661,7 +680,7 @@ __device__ void group_bulk(const Tables& T, int lane, DeepMsg* msgs, uint64_t S,
       for (int k = 0; k < 16; ++k) le[k] = 0;
       if (live) load_block_le<kAligned16>(q + 64 * ((st + 1) * G + (uint64_t)i), le);
     }
-    if (any_sha) {
+    if constexpr (kSha) {
       auto block = [&]() {
         uint32_t s[5] = {hv[0], hv[1], hv[2], hv[3], hv[4]};
         ChainRegs<0>::run(s, x);  // real in lane m*G+j of every job m at iteration j
@@ -682,11 +701,19 @@ __device__ void group_bulk(const Tables& T, int lane, DeepMsg* msgs, uint64_t S,
   if (live && i == 0) {  // joint jobs only
     DeepMsg& W = msgs[m];
 #pragma unroll
-    for (int k = 0; k < 5; ++k) W.h[k] = any_sha ? hv[k] : W.h[k];
+    for (int k = 0; k < 5; ++k) W.h[k] = kSha ? hv[k] : W.h[k];
     W.crc_raw = crc_raw;
     W.done += S * G;
   }
   wave_lds_sync();
+}
+
+template <int G, bool kAligned16>
+__device__ void group_bulk_any(const Tables& T, const PosTables& P, int lane, DeepMsg* msgs, uint64_t S, bool any_sha,
+                               bool any_crc) {
+  if (any_sha && any_crc) group_bulk<G, kAligned16, true, true>(T, P, lane, msgs, S);
+  else if (any_sha) group_bulk<G, kAligned16, true, false>(T, P, lane, msgs, S);
+  else group_bulk<G, kAligned16, false, true>(T, P, lane, msgs, S);
 }
 
 
@@ -697,9 +724,9 @@ __global__ __launch_bounds__(64 * kDeepWaves, 1) void group_kernel(const efes_jo
   static_assert(kJobs <= kGroupMaxJobs, "LDS holds kGroupMaxJobs jobs per wave");
   __shared__ __attribute__((aligned(16))) DeepLDS L;
   {
-    const uint4* src = reinterpret_cast<const uint4*>(tabs);
+    const uint4* src = reinterpret_cast<const uint4*>(tabs);  // Tables then PosTables
     uint4* dst = reinterpret_cast<uint4*>(&L.tab);
-    for (int i = threadIdx.x; i < (int)(sizeof(Tables) / 16); i += blockDim.x) dst[i] = src[i];
+    for (int i = threadIdx.x; i < (int)((sizeof(Tables) + sizeof(PosTables)) / 16); i += blockDim.x) dst[i] = src[i];
   }
   __syncthreads();
   const int wave = (int)uniform32(threadIdx.x >> 6);
@@ -743,8 +770,8 @@ __global__ __launch_bounds__(64 * kDeepWaves, 1) void group_kernel(const efes_jo
       if (lane == 0) msgs[m].joint = M.live && (M.nbulk - M.done) / G > 0 ? 1u : 0u;
     }
     wave_lds_sync();
-    if (all16) group_bulk<G, true>(L.tab, lane, msgs, S, any_sha, any_crc);
-    else group_bulk<G, false>(L.tab, lane, msgs, S, any_sha, any_crc);
+    if (all16) group_bulk_any<G, true>(L.tab, L.pos, lane, msgs, S, any_sha, any_crc);
+    else group_bulk_any<G, false>(L.tab, L.pos, lane, msgs, S, any_sha, any_crc);
   }
 
   // ---- per job: left-over blocks, tail, Sum, write-back

@@ -618,9 +618,9 @@ __global__ __launch_bounds__(128 * kPipeJobs, 1) void deep_kernel(const efes_job
 // ================================================================== grouped DEEP kernel
 // k = 64/G jobs per wave, G lanes (= G consecutive blocks per super-step) per job.  For
 // batches with more long jobs than SIMDs: the chain instructions are shared by the k jobs
-// (lane m*G+i runs block i of job m), so a super-step of 410 G + 770 instructions advances
-// k jobs by G blocks each: (410 G + 770)/64 instructions per block of issue work (DEEP: 422)
-// at a per-job latency of 410 + 770/G per block (WIDE: 740 at a slower issue rate).
+// (lane m*G+i runs block i of job m), so a super-step of 410 G + 715 instructions advances
+// k jobs by G blocks each: (410 G + 715)/64 instructions per block of issue work (DEEP: 422)
+// at a per-job latency of 410 + 715/G per block (WIDE: 740 at a slower issue rate).
 // DESIGN.md §4 "grouped DEEP".
 //
 // Phases per wave: the head of every job (sequential, state parked in LDS); joint rounds in
@@ -748,7 +748,7 @@ __global__ __launch_bounds__(64 * kDeepWaves, 1) void group_kernel(const efes_jo
   // ---- joint rounds: while two or more jobs have >= G bulk blocks left, they advance together
   // by S*G blocks, S = the smallest of their floor(left/G) (so a wave lasts as long as its
   // longest job, whatever the mix of lengths); a job left alone finishes on the one-job path
-  // (422 instructions per block instead of (410 G + 770)/G).
+  // (422 instructions per block instead of (410 G + 715)/G).
   for (int round = 0; round < kJobs; ++round) {
     uint64_t S = ~0ull;
     int joiners = 0;

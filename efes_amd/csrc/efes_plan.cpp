@@ -6,7 +6,7 @@
 // Per 64-B block, in SIMD cycles (MI355X, measured: DESIGN.md §4 "grouped DEEP"):
 //   shape                      latency of one job           SIMD work per job
 //   DEEP  (one wave per job)   422 x 4.1                    422 x 4.1
-//   GROUPn (64/n jobs / wave)  (410 + 770/n) x 4.1          (410 n + 770)/64 x 4.1
+//   GROUPn (64/n jobs / wave)  (410 + 715/n) x 4.1          (410 n + 715)/64 x 4.1
 //   WIDE  (one lane per job)   740 x 5.1                    740/64 x 5.1 (/1.06 once SIMDs hold 2+ waves)
 // A DEEP/GROUP wave issues at ~4.1 cycles per instruction alone and gains almost nothing from
 // a second wave on its SIMD (1.06x), so where a long job's wave lands matters: the plan can
@@ -41,11 +41,11 @@ constexpr int kWideLanes = 0;       // "shape" id of WIDE in the search
 
 double latency(int g) {  // cycles per block of one job
   if (g == kWideLanes) return 740.0 * kCpiWide;
-  return (g == 64 ? 422.0 : 410.0 + 770.0 / g) * kCpiDeep;
+  return (g == 64 ? 422.0 : 410.0 + 715.0 / g) * kCpiDeep;
 }
 double work(int g, bool crowded) {  // SIMD cycles per block per job
   if (g == kWideLanes) return 740.0 / 64.0 * kCpiWide / (crowded ? kWideShare : 1.0);
-  return (g == 64 ? 422.0 : (410.0 * g + 770.0) / 64.0) * kCpiDeep;
+  return (g == 64 ? 422.0 : (410.0 * g + 715.0) / 64.0) * kCpiDeep;
 }
 double waves(int g, double jobs) { return std::ceil(jobs / (g == kWideLanes ? 64.0 : 64.0 / g)); }
 int mode_of(int g) {

@@ -234,7 +234,7 @@ int efes_auto_mode(const efes_ctx* ctx, uint32_t njobs) {
 }
 
 int efes_hash_submit_mode(efes_ctx* ctx, const efes_job* jobs, uint32_t njobs, void* stream, int mode) {
-  if (!ctx || (!jobs && njobs)) return EFES_ERR_ARG;
+  if (!ctx || (!jobs && njobs) || njobs > EFES_MAX_JOBS) return EFES_ERR_ARG;
   if (njobs == 0) return EFES_OK;
   if (mode == EFES_MODE_AUTO) mode = efes_auto_mode(ctx, njobs);
   DeviceGuard g(ctx->device);

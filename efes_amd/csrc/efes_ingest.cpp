@@ -166,7 +166,7 @@ static int hash_host_mapped(efes_ctx* ctx, const efes_job* jobs, uint32_t n, efe
 }
 
 int efes_hash_host(efes_ctx* ctx, const efes_job* jobs, uint32_t n, uint64_t segment_bytes, efes_host_stats* stats) {
-  if (!ctx || (!jobs && n)) return EFES_ERR_ARG;
+  if (!ctx || (!jobs && n) || n > EFES_MAX_JOBS) return EFES_ERR_ARG;
   if (stats) memset(stats, 0, sizeof *stats);
   if (n == 0) return EFES_OK;
   for (uint32_t i = 0; i < n; ++i)

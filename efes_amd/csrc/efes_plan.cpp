@@ -75,7 +75,7 @@ struct Cand {
 extern "C" {
 
 int efes_plan_batch(efes_ctx* ctx, const uint64_t* lengths, uint32_t n, uint32_t* order, efes_plan* plan) {
-  if (!plan || (n && (!lengths || !order))) return EFES_ERR_ARG;
+  if (!plan || (n && (!lengths || !order)) || n > EFES_MAX_JOBS) return EFES_ERR_ARG;
   *plan = efes_plan{};
   plan->njobs = n;
   if (n == 0) return EFES_OK;
@@ -208,7 +208,8 @@ int efes_plan_batch(efes_ctx* ctx, const uint64_t* lengths, uint32_t n, uint32_t
 }
 
 int efes_hash_submit_plan(efes_ctx* ctx, const efes_job* jobs, const efes_plan* plan, void* stream) {
-  if (!ctx || !plan || plan->nparts > EFES_PLAN_MAX_PARTS || (plan->njobs && !jobs)) return EFES_ERR_ARG;
+  if (!ctx || !plan || plan->nparts > EFES_PLAN_MAX_PARTS || (plan->njobs && !jobs) || plan->njobs > EFES_MAX_JOBS)
+    return EFES_ERR_ARG;
   uint64_t total = 0;
   for (uint32_t i = 0; i < plan->nparts; ++i) {
     const efes_plan_part& p = plan->part[i];

@@ -113,6 +113,10 @@ typedef struct efes_job {
 #define EFES_MODE_GROUP16 5
 #define EFES_MODE_GROUP32 6
 
+/* Largest job count of one submit / plan / host batch (larger counts: EFES_ERR_ARG; split the
+ * batch).  Keeps every grid size and lane index of the kernels within 32 bits. */
+#define EFES_MAX_JOBS (1u << 30)
+
 /* Enqueue njobs jobs (the job array itself in DEVICE memory) on `stream` (a
  * hipStream_t; NULL = the context stream).  Asynchronous; returns launch errors only. */
 int efes_hash_submit(efes_ctx* ctx, const efes_job* jobs_device, uint32_t njobs, void* stream);

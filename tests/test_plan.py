@@ -87,3 +87,16 @@ def test_force_override_rejects_too_many_parts(monkeypatch):
     monkeypatch.setenv("EFES_PLAN_FORCE", "4:10,8:10,16:10")
     _, plan = plan_batch([MiB] * 3000)
     assert plan.parts() == model.parts()
+
+
+def test_batch_larger_than_max_jobs_is_rejected():
+    """EFES_MAX_JOBS (efes_hash.h): a count beyond it is EFES_ERR_ARG before anything is read."""
+    import ctypes
+
+    from efes_amd._lib import EFES_ERR_ARG as ERR_ARG, Plan, lib
+
+    one = (ctypes.c_uint64 * 1)(64)
+    order = (ctypes.c_uint32 * 1)()
+    plan = Plan()
+    assert lib().efes_plan_batch(None, one, (1 << 30) + 1, order, ctypes.byref(plan)) == ERR_ARG
+    assert lib().efes_plan_batch(None, one, 1, order, ctypes.byref(plan)) == 0

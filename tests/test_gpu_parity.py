@@ -810,3 +810,67 @@ def test_planned_batch_random_lengths(env, oracle):
     for i in range(n):
         d = host[int(offsets[i]):int(offsets[i]) + int(lengths[i])].tobytes()
         assert shas[i] == hashlib.sha1(d).hexdigest() and crcs[i] == zlib.crc32(d), (i, int(lengths[i]))
+
+
+def _spot_check(env, buf, offsets, lengths, shas, crcs, picks):
+    """hashlib / zlib on chunks copied back from the device (chunks alias a pool: bytes differ)."""
+    for i in picks:
+        o, n = int(offsets[i]), int(lengths[i])
+        d = buf[o:o + n].cpu().numpy().tobytes()
+        assert shas[i] == hashlib.sha1(d).hexdigest() and crcs[i] == zlib.crc32(d), (i, n)
+
+
+def test_full_size_metric_config_all_shapes_agree(env):
+    """BASELINE configs[2] at full size (1024 x 4 MiB, device-filled like bench.py): DEEP, GROUP32
+    and WIDE (three different kernels, lane layouts and CRC schemes) give identical digests, and a
+    sample matches hashlib/zlib.  Size-independent property at the metric's own size."""
+    from efes_amd._lib import MODE_GROUP
+    torch = env["torch"]
+    n, size = 1024, 4 << 20
+    buf = torch.empty(n * size, dtype=torch.uint8, device="cuda:0")
+    env["ctx"].fill_synthetic(buf.data_ptr(), buf.numel(), 0xEFE5, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    offsets, lengths = np.arange(n, dtype=np.uint64) * size, np.full(n, size, np.uint64)
+    b = env["DeviceBatch"](buf.data_ptr(), offsets, lengths, fresh=True, ctx=env["ctx"])
+    got = {}
+    for name, mode in [("deep", env["efes"].MODE_DEEP), ("group32", MODE_GROUP[32]), ("wide", env["efes"].MODE_WIDE)]:
+        b.reset()
+        b.run(mode)
+        assert (b.status_host() == 0).all(), name
+        got[name] = (b.sha1_hex(), b.crc_sum().copy())
+    assert got["deep"][0] == got["group32"][0] == got["wide"][0]
+    assert (got["deep"][1] == got["group32"][1]).all() and (got["deep"][1] == got["wide"][1]).all()
+    assert len(set(got["deep"][0])) == n  # distinct data per chunk
+    _spot_check(env, buf, offsets, lengths, got["deep"][0], got["deep"][1], [0, 1, 511, 1022, 1023])
+
+
+def test_full_size_mixed_config_plan_equals_wide(env):
+    """BASELINE configs[3] at full size (65 536 chunks of the eleven ChunkSize classes 64K..64M,
+    752 GiB aliasing an 8 GiB pool, seed 7 as bench.py): the planner's concurrent parts (grouped
+    DEEP on reserved CUs + WIDE) and an all-WIDE run agree on every digest; one chunk per class
+    (and the longest) matches hashlib/zlib."""
+    from efes_amd.batch import MODE_PLAN
+    from efes_amd.chunksize import MIXED_CLASSES
+    torch = env["torch"]
+    pool = 8 << 30
+    buf = torch.empty(pool, dtype=torch.uint8, device="cuda:0")
+    env["ctx"].fill_synthetic(buf.data_ptr(), pool, 0xEFE5, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    rng = np.random.default_rng(7)
+    sizes = np.asarray(MIXED_CLASSES, dtype=np.uint64)[rng.integers(0, len(MIXED_CLASSES), 65536)]
+    sizes = np.sort(sizes)[::-1].copy()
+    offs = (rng.integers(0, (pool - sizes.astype(np.int64)) // 256 + 1) * 256).astype(np.uint64)
+    b = env["DeviceBatch"](buf.data_ptr(), offs, sizes, fresh=True, ctx=env["ctx"])
+    b.make_plan()
+    assert len(b.plan.parts()) >= 2  # a real multi-part plan
+    b.run(MODE_PLAN)
+    assert (b.status_host() == 0).all()
+    plan_sha, plan_crc = b.sha1_hex(), b.crc_sum().copy()
+    b.reset()
+    b.run(env["efes"].MODE_WIDE)
+    assert (b.status_host() == 0).all()
+    assert b.sha1_hex() == plan_sha and (b.crc_sum() == plan_crc).all()
+    picks = [0] + [int(np.argmax(sizes == c)) for c in MIXED_CLASSES if (sizes == c).any()]
+    _spot_check(env, buf, offs, sizes, plan_sha, plan_crc, picks)
+    del buf
+    torch.cuda.empty_cache()

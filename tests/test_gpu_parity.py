@@ -874,3 +874,30 @@ def test_full_size_mixed_config_plan_equals_wide(env):
     _spot_check(env, buf, offs, sizes, plan_sha, plan_crc, picks)
     del buf
     torch.cuda.empty_cache()
+
+
+def test_full_size_ingest_launch_wide_equals_group4(env):
+    """One BASELINE configs[4] launch at full size (196 608 x 4 MiB, chunks aliasing pool slots as
+    bench.py's ingest leg does): WIDE (the shape AUTO picks) and GROUP4 agree on every digest,
+    chunks that alias the same slot get the same digest, and a sample matches hashlib/zlib."""
+    from efes_amd._lib import MODE_GROUP
+    torch = env["torch"]
+    chunk, slots, m = 4 << 20, 2048, 196608
+    buf = torch.empty(slots * chunk, dtype=torch.uint8, device="cuda:0")
+    env["ctx"].fill_synthetic(buf.data_ptr(), buf.numel(), 0xEFE5, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    idx = (np.arange(m, dtype=np.uint64) + np.uint64(7919)) % np.uint64(slots)
+    offs, lengths = idx * np.uint64(chunk), np.full(m, chunk, np.uint64)
+    b = env["DeviceBatch"](buf.data_ptr(), offs, lengths, fresh=True, ctx=env["ctx"])
+    assert env["hashing"].lib().efes_auto_mode(env["ctx"].handle, m) == env["efes"].MODE_WIDE
+    b.run(env["efes"].MODE_WIDE)
+    assert (b.status_host() == 0).all()
+    wide_sha, wide_crc = b.sha1_hex(), b.crc_sum().copy()
+    b.reset()
+    b.run(MODE_GROUP[4])
+    assert (b.status_host() == 0).all()
+    assert b.sha1_hex() == wide_sha and (b.crc_sum() == wide_crc).all()
+    for i in (0, 1, 2047, 100000):
+        assert wide_sha[i] == wide_sha[i + slots] and wide_crc[i] == wide_crc[i + slots]
+    assert len(set(wide_sha)) == slots
+    _spot_check(env, buf, offs, lengths, wide_sha, wide_crc, [0, 1, 65535, m - 1])

@@ -872,20 +872,35 @@ __device__ __forceinline__ void wide_step(const uint32_t (&le)[16], const uint32
 
 // Whole blocks of one lane's message: block b is hashed (SHA-1 rounds and CRC steps woven
 // together) while blocks b+1 and b+2 are in flight (three 16-word buffers, loop unrolled by
-// three so the buffers keep their registers).  The trip count is the wave's longest message
-// (`nmax`, uniform), so the loads are unconditional and the compiler's vmcnt waits are exact;
-// lanes past their own last block load a harmless `dummy` block and do not commit.  kSha/kCrc
-// are wave-uniform template flags; a lane that needs only one of the two computes both and
-// never stores the other.  Jobs sorted by length keep the lanes of a wave equally long.
+// three so the buffers keep their registers).  Two phases:
+//  * uniform: while every lane of the wave still has the blocks being hashed and prefetched
+//    (b+4 < nmin, the wave's shortest message), loads are unconditional and every lane
+//    commits -- no per-lane selects (8 VALU per block fewer than the ragged phase);
+//  * ragged: up to the wave's longest message (`nmax`, uniform), so the loads stay
+//    unconditional and the compiler's vmcnt waits exact; lanes past their own last block
+//    load a harmless `dummy` block and do not commit.
+// kSha/kCrc are wave-uniform template flags; a lane that needs only one of the two computes
+// both and never stores the other.  Jobs sorted by length keep the lanes of a wave equally long.
 template <bool kAligned16, bool kSha, bool kCrc>
-__device__ __forceinline__ void wide_bulk(const uint8_t* q, uint64_t nbulk, uint64_t nmax, const uint8_t* dummy,
-                                          const uint32_t (&t)[8][256], uint32_t (&h)[5], uint32_t& crc_raw) {
+__device__ __forceinline__ void wide_bulk(const uint8_t* q, uint64_t nbulk, uint64_t nmin, uint64_t nmax,
+                                          const uint8_t* dummy, const uint32_t (&t)[8][256], uint32_t (&h)[5],
+                                          uint32_t& crc_raw) {
   auto src = [&](uint64_t b) { return b < nbulk ? q + 64 * b : dummy; };
   uint32_t A[16], B[16], C[16];
   if (nmax == 0) return;
   load_block_le<kAligned16>(src(0), A);
   load_block_le<kAligned16>(src(1), B);
-  for (uint64_t b = 0; b < nmax; b += 3) {
+  uint64_t b = 0;
+  for (; b + 4 < nmin; b += 3) {  // uniform phase: blocks b..b+4 exist in every lane
+    const uint8_t* qb = q + 64 * b;
+    load_block_le<kAligned16>(qb + 128, C);
+    wide_step<kSha, kCrc>(A, t, h, crc_raw, true);
+    load_block_le<kAligned16>(qb + 192, A);
+    wide_step<kSha, kCrc>(B, t, h, crc_raw, true);
+    load_block_le<kAligned16>(qb + 256, B);
+    wide_step<kSha, kCrc>(C, t, h, crc_raw, true);
+  }
+  for (; b < nmax; b += 3) {  // ragged phase (A, B hold blocks b, b+1 or the dummy)
     load_block_le<kAligned16>(src(b + 2), C);
     wide_step<kSha, kCrc>(A, t, h, crc_raw, b < nbulk);
     if (b + 1 >= nmax) break;
@@ -897,12 +912,24 @@ __device__ __forceinline__ void wide_bulk(const uint8_t* q, uint64_t nbulk, uint
   }
 }
 template <bool kAligned16>
-__device__ __forceinline__ void wide_bulk_any(const uint8_t* q, uint64_t nbulk, uint64_t nmax, const uint8_t* dummy,
-                                              bool any_sha, bool any_crc, const uint32_t (&t)[8][256],
-                                              uint32_t (&h)[5], uint32_t& crc_raw) {
-  if (any_sha && any_crc) wide_bulk<kAligned16, true, true>(q, nbulk, nmax, dummy, t, h, crc_raw);
-  else if (any_sha) wide_bulk<kAligned16, true, false>(q, nbulk, nmax, dummy, t, h, crc_raw);
-  else if (any_crc) wide_bulk<kAligned16, false, true>(q, nbulk, nmax, dummy, t, h, crc_raw);
+__device__ __forceinline__ void wide_bulk_any(const uint8_t* q, uint64_t nbulk, uint64_t nmin, uint64_t nmax,
+                                              const uint8_t* dummy, bool any_sha, bool any_crc,
+                                              const uint32_t (&t)[8][256], uint32_t (&h)[5], uint32_t& crc_raw) {
+  if (any_sha && any_crc) wide_bulk<kAligned16, true, true>(q, nbulk, nmin, nmax, dummy, t, h, crc_raw);
+  else if (any_sha) wide_bulk<kAligned16, true, false>(q, nbulk, nmin, nmax, dummy, t, h, crc_raw);
+  else if (any_crc) wide_bulk<kAligned16, false, true>(q, nbulk, nmin, nmax, dummy, t, h, crc_raw);
+}
+
+// Wave-wide minimum of a per-lane 64-bit value over the lanes where `use` holds (uniform
+// result; ~0 when no lane does).
+__device__ __forceinline__ uint64_t wave_min64(uint64_t v, bool use) {
+  v = use ? v : ~0ull;
+#pragma unroll
+  for (int k = 1; k < 64; k <<= 1) {
+    const uint64_t o = (uint64_t)__shfl_xor((unsigned long long)v, k);
+    v = o < v ? o : v;
+  }
+  return uniform64(v);
 }
 
 // Wave-wide maximum of a per-lane 64-bit value (uniform result).
@@ -986,9 +1013,11 @@ __global__ __launch_bounds__(64 * kWideWaves, 2) void wide_kernel(const efes_job
   const bool all16 = __all(!go || (reinterpret_cast<uintptr_t>(q) & 15) == 0);
   const bool any_sha = __any(do_sha), any_crc = __any(do_crc);  // wave-uniform
   const uint64_t nmax = wave_max64(nbulk);
+  // the shortest message over ALL lanes (a lane without a job has nbulk 0: no uniform phase)
+  const uint64_t nmin = wave_min64(nbulk, true);
   const uint8_t* dummy = reinterpret_cast<const uint8_t*>(tabs);  // 36 KiB of valid device memory
-  if (all16) wide_bulk_any<true>(q, nbulk, nmax, dummy, any_sha, any_crc, L.slice8, h, crc_raw);
-  else wide_bulk_any<false>(q, nbulk, nmax, dummy, any_sha, any_crc, L.slice8, h, crc_raw);
+  if (all16) wide_bulk_any<true>(q, nbulk, nmin, nmax, dummy, any_sha, any_crc, L.slice8, h, crc_raw);
+  else wide_bulk_any<false>(q, nbulk, nmin, nmax, dummy, any_sha, any_crc, L.slice8, h, crc_raw);
 
   // ---- tail
   const uint64_t tpos = pos + (nbulk << 6);

@@ -618,9 +618,9 @@ __global__ __launch_bounds__(128 * kPipeJobs, 1) void deep_kernel(const efes_job
 // ================================================================== grouped DEEP kernel
 // k = 64/G jobs per wave, G lanes (= G consecutive blocks per super-step) per job.  For
 // batches with more long jobs than SIMDs: the chain instructions are shared by the k jobs
-// (lane m*G+i runs block i of job m), so a super-step of 410 G + 715 instructions advances
-// k jobs by G blocks each: (410 G + 715)/64 instructions per block of issue work (DEEP: 422)
-// at a per-job latency of 410 + 715/G per block (WIDE: 740 at a slower issue rate).
+// (lane m*G+i runs block i of job m), so a super-step of 410 G + ~700 instructions advances
+// k jobs by G blocks each: (410 G + ~700)/64 instructions per block of issue work (DEEP: 422)
+// at a per-job latency of 410 + ~700/G per block (WIDE: 740 at a slower issue rate).
 // DESIGN.md §4 "grouped DEEP".
 //
 // Phases per wave: the head of every job (sequential, state parked in LDS); joint rounds in
@@ -653,13 +653,12 @@ __device__ void group_bulk(const Tables& T, const PosTables& P, int lane, DeepMs
   const uint8_t* q = M.q + 64 * M.done;
   uint32_t hv[5] = {M.h[0], M.h[1], M.h[2], M.h[3], M.h[4]}, hs[5] = {0, 0, 0, 0, 0};
   uint32_t crc_raw = M.crc_raw;
-  uint32_t le[16];
-#pragma unroll
-  for (int k = 0; k < 16; ++k) le[k] = 0;
-  if (live) load_block_le<kAligned16>(q + 64 * (uint64_t)i, le);
-  for (uint64_t st = 0; st < S; ++st) {
+  // One super-step: CRC + schedule of this lane's block `cur`, the prefetch of the next
+  // super-step's block into `nxt` (exec-masked: a lane of a job outside this round loads
+  // nothing; zeroed first so the compiler keeps the prefetch a whole chain ahead), the chain.
+  auto super_step = [&](const uint32_t (&cur)[16], uint32_t (&nxt)[16], uint64_t st) {
     if constexpr (kCrc) {
-      uint32_t r = crc_block_pos(P.pos, le);  // raw CRC of this lane's block, register 0
+      uint32_t r = crc_block_pos(P.pos, cur);  // raw CRC of this lane's block, register 0
 #pragma unroll
       for (int k = 0; k < kLG; ++k) {  // crc(A||B) = shift(crc(A), |B|) ^ crc(B) within the job's G lanes
         const uint32_t o = __shfl_xor(r, 1 << k);
@@ -672,13 +671,13 @@ __device__ void group_bulk(const Tables& T, const PosTables& P, int lane, DeepMs
     if constexpr (kSha) {
       uint32_t w[16];
 #pragma unroll
-      for (int k = 0; k < 16; ++k) w[k] = bswap(le[k]);
+      for (int k = 0; k < 16; ++k) w[k] = bswap(cur[k]);
       expand_wk(w, x);
     }
     if (st + 1 < S) {
 #pragma unroll
-      for (int k = 0; k < 16; ++k) le[k] = 0;
-      if (live) load_block_le<kAligned16>(q + 64 * ((st + 1) * G + (uint64_t)i), le);
+      for (int k = 0; k < 16; ++k) nxt[k] = 0;
+      if (live) load_block_le<kAligned16>(q + 64 * ((st + 1) * G + (uint64_t)i), nxt);
     }
     if constexpr (kSha) {
       auto block = [&]() {
@@ -695,6 +694,23 @@ __device__ void group_bulk(const Tables& T, const PosTables& P, int lane, DeepMs
       // the job's chaining value is in its last lane: back to all G lanes (its first one needs it)
 #pragma unroll
       for (int k = 0; k < 5; ++k) hv[k] = (uint32_t)__shfl((int)hs[k], lane | (G - 1));
+    }
+  };
+  uint32_t A[16], B[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) A[k] = 0;
+  if (live) load_block_le<kAligned16>(q + 64 * (uint64_t)i, A);
+  if constexpr (G <= 8) {  // two buffers, unrolled by two: no register copies of the prefetch
+    for (uint64_t st = 0; st < S; st += 2) {
+      super_step(A, B, st);
+      if (st + 1 >= S) break;
+      super_step(B, A, st + 1);
+    }
+  } else {  // (GROUP16/32: one buffer; the unrolled chain is already 16-32 blocks of code)
+    for (uint64_t st = 0; st < S; ++st) {
+      super_step(A, B, st);
+#pragma unroll
+      for (int k = 0; k < 16; ++k) A[k] = B[k];
     }
   }
   wave_lds_sync();
@@ -748,7 +764,7 @@ __global__ __launch_bounds__(64 * kDeepWaves, 1) void group_kernel(const efes_jo
   // ---- joint rounds: while two or more jobs have >= G bulk blocks left, they advance together
   // by S*G blocks, S = the smallest of their floor(left/G) (so a wave lasts as long as its
   // longest job, whatever the mix of lengths); a job left alone finishes on the one-job path
-  // (422 instructions per block instead of (410 G + 715)/G).
+  // (422 instructions per block instead of (410 G + ~700)/G).
   for (int round = 0; round < kJobs; ++round) {
     uint64_t S = ~0ull;
     int joiners = 0;

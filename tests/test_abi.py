@@ -176,3 +176,10 @@ def test_auto_mode_by_job_count(efes_lib):
     want = {1: efes_lib.MODE_DEEP, 1024: efes_lib.MODE_DEEP, 1025: G[32], 2048: G[32], 4096: G[16], 8192: G[8],
             8193: G[4], 24576: G[4], 24577: efes_lib.MODE_WIDE, 131072: efes_lib.MODE_WIDE}
     assert {n: L.efes_auto_mode(None, n) for n in want} == want
+
+
+def test_integration_doc_covers_every_declared_symbol():
+    """Every entry point of include/efes_hash.h appears in INTEGRATION.md (cgo binding or table)."""
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    missing = [n for n in declared_functions() if not re.search(r"\b%s\b" % n, doc)]
+    assert not missing, missing

@@ -14,6 +14,12 @@
 // Tail-buffer bytes x/nx/len are replayed on the host per Write (efes::replay_write), so an
 // exported state is byte-identical to what Go's MarshalText would write after the same
 // Write calls, stale bytes included; h and crc come from the device.
+//
+// The per-upload state slots live in pinned, device-mapped host memory: the kernels read and
+// write an upload's 104 + 4 bytes of state once per job over PCIe, and the sync points read
+// them in place.  Sum is a zero-length FINALIZE job of the same dispatcher (so the Sums of many
+// requests share launches with everyone's chunks) writing the 24-byte digest pair into the
+// slot.  No sync point issues a copy or a launch of its own.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
@@ -31,9 +37,10 @@
 using efes::DeviceGuard;
 
 namespace {
-// Device slot of one upload: sha1 state 104 | crc 4 | pad | sum 24 | status 4 | pad | job 56.
+// State slot of one upload (pinned, device-mapped): sha1 state 104 | crc 4 | pad | sum 24 | status 4.
 constexpr size_t kDevStateBytes = 256;
-constexpr size_t kOffCrc = 104, kOffSum = 112, kOffStatus = 136, kOffJob = 144;
+constexpr size_t kOffCrc = 104, kOffSum = 112, kOffStatus = 136;
+constexpr uint32_t kNoChunk = 0xffffffffu;  // a Pending that is a Sum (FINALIZE, no bytes)
 }  // namespace
 
 struct efes_upload {
@@ -51,7 +58,7 @@ struct efes_upload {
 
 struct Pending {
   efes_upload* u;
-  uint32_t slot;
+  uint32_t slot;  // staging chunk, or kNoChunk for a Sum
   uint64_t len;
 };
 
@@ -67,10 +74,11 @@ struct efes_queue {
   uint32_t nchunks = 0, max_uploads = 0;
   uint8_t* h_slab = nullptr;       // pinned, device-mapped staging, nchunks x chunk
   uint8_t* z_slab = nullptr;       // the device address of h_slab: kernels read it over PCIe
-  uint8_t* d_states = nullptr;     // max_uploads x kDevStateBytes
+  uint8_t* h_states = nullptr;     // max_uploads x kDevStateBytes, pinned + device-mapped
+  uint8_t* z_states = nullptr;     // the device address of h_states
   efes_job* h_jobs = nullptr;      // pinned, 2 halves x nchunks
   efes_job* d_jobs = nullptr;
-  hipStream_t stream = nullptr, ctl = nullptr;
+  hipStream_t stream = nullptr;
   std::mutex mu;
   std::condition_variable work, freed;
   std::vector<uint32_t> free_chunks, free_states;
@@ -93,7 +101,7 @@ void efes_queue::retire(Batch& b, std::unique_lock<std::mutex>& lk) {  // mu hel
   lk.lock();
   if (!ok && fault == EFES_OK) fault = EFES_ERR_DEVICE_FAULT;
   for (const Pending& p : b.items) {
-    free_chunks.push_back(p.slot);
+    if (p.slot != kNoChunk) free_chunks.push_back(p.slot);
     if (!ok) p.u->latched = EFES_ERR_DEVICE_FAULT;
     if (--p.u->inflight == 0) p.u->done.notify_all();
   }
@@ -142,15 +150,16 @@ void efes_queue::run() {
     efes_job* dj = d_jobs + (size_t)b.jobs_half * nchunks;
     for (size_t i = 0; i < b.items.size(); ++i) {
       const Pending& p = b.items[i];
-      uint8_t* st = d_states + (size_t)p.u->dslot * kDevStateBytes;
+      uint8_t* st = z_states + (size_t)p.u->dslot * kDevStateBytes;
+      const bool sum = p.slot == kNoChunk;  // Sum: works on a copy (sha1.go:82-87), state unchanged
       efes_job& j = hj[i];
-      j.data = z_slab + (size_t)p.slot * chunk;
-      j.length = p.len;
+      j.data = sum ? nullptr : z_slab + (size_t)p.slot * chunk;
+      j.length = sum ? 0 : p.len;
       j.sha1 = (p.u->hashes & EFES_HASH_SHA1) ? reinterpret_cast<efes_sha1_state*>(st) : nullptr;
       j.crc32 = (p.u->hashes & EFES_HASH_CRC32) ? reinterpret_cast<efes_crc32_state*>(st + kOffCrc) : nullptr;
-      j.sum = nullptr;
+      j.sum = sum ? st + kOffSum : nullptr;
       j.status = reinterpret_cast<int32_t*>(st + kOffStatus);
-      j.flags = 0;
+      j.flags = sum ? EFES_JOB_FINALIZE : 0u;
       j._reserved = 0;
     }
     lk.unlock();  // callers keep staging while this batch is copied and launched
@@ -171,7 +180,7 @@ void efes_queue::run() {
       if (b.ev) (void)hipEventDestroy(b.ev);
       if (fault == EFES_OK) fault = rc;
       for (const Pending& p : b.items) {
-        free_chunks.push_back(p.slot);
+        if (p.slot != kNoChunk) free_chunks.push_back(p.slot);
         p.u->latched = rc;
         if (--p.u->inflight == 0) p.u->done.notify_all();
       }
@@ -222,12 +231,13 @@ int efes_queue_create(efes_ctx* ctx, uint64_t chunk_bytes, uint32_t max_chunks, 
   DeviceGuard g(ctx->device);
   hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&q->h_slab), q->chunk * max_chunks, hipHostMallocMapped);
   if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void**>(&q->z_slab), q->h_slab, 0);
-  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&q->d_states), kDevStateBytes * max_uploads);
+  if (e == hipSuccess)
+    e = hipHostMalloc(reinterpret_cast<void**>(&q->h_states), kDevStateBytes * max_uploads, hipHostMallocMapped);
+  if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void**>(&q->z_states), q->h_states, 0);
   if (e == hipSuccess)
     e = hipHostMalloc(reinterpret_cast<void**>(&q->h_jobs), 2 * sizeof(efes_job) * max_chunks, hipHostMallocDefault);
   if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&q->d_jobs), 2 * sizeof(efes_job) * max_chunks);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&q->stream, hipStreamNonBlocking);
-  if (e == hipSuccess) e = hipStreamCreateWithFlags(&q->ctl, hipStreamNonBlocking);
   if (e != hipSuccess) {
     efes_queue_destroy(q);
     return EFES_ERR_HIP;
@@ -256,13 +266,11 @@ void efes_queue_destroy(efes_queue* q) {
   }
   DeviceGuard g(q->ctx->device);
   if (q->stream) (void)hipStreamSynchronize(q->stream);
-  if (q->ctl) (void)hipStreamSynchronize(q->ctl);
   if (q->h_slab) (void)hipHostFree(q->h_slab);
-  if (q->d_states) (void)hipFree(q->d_states);
+  if (q->h_states) (void)hipHostFree(q->h_states);
   if (q->h_jobs) (void)hipHostFree(q->h_jobs);
   if (q->d_jobs) (void)hipFree(q->d_jobs);
   if (q->stream) (void)hipStreamDestroy(q->stream);
-  if (q->ctl) (void)hipStreamDestroy(q->ctl);
   delete q;
 }
 
@@ -289,18 +297,12 @@ int efes_upload_open(efes_queue* q, uint32_t hashes, const efes_sha1_state* sha1
     memset(&u->shadow, 0, sizeof u->shadow);
     efes_sha1_state_init(&u->shadow);  // NewSha1 (sha1.go:48-52)
   }
-  uint8_t init[kDevStateBytes] = {};
-  memcpy(init, &u->shadow, sizeof u->shadow);
+  // the slot is not in use by any kernel (its previous upload closed after its last job)
+  uint8_t* st = q->h_states + (size_t)u->dslot * kDevStateBytes;
+  memset(st, 0, kDevStateBytes);
+  memcpy(st, &u->shadow, sizeof u->shadow);
   const uint32_t c = crc ? crc->crc : 0u;  // NewCRC32IEEE
-  memcpy(init + kOffCrc, &c, 4);
-  DeviceGuard g(q->ctx->device);
-  hipError_t e = hipMemcpyAsync(q->d_states + (size_t)u->dslot * kDevStateBytes, init, sizeof init,
-                                hipMemcpyHostToDevice, q->ctl);
-  if (e == hipSuccess) e = hipStreamSynchronize(q->ctl);
-  if (e != hipSuccess) {
-    efes_upload_close(u);
-    return EFES_ERR_HIP;
-  }
+  memcpy(st + kOffCrc, &c, 4);
   *out = u;
   return EFES_OK;
 }
@@ -357,15 +359,9 @@ int efes_upload_flush(efes_upload* u) {
 
 int efes_upload_state(efes_upload* u, efes_sha1_state* sha1, efes_crc32_state* crc) {
   if (!u) return EFES_ERR_ARG;
-  int rc = wait_idle(u);
+  int rc = wait_idle(u);  // after this no job of the upload is in flight: the slot is final
   if (rc) return rc;
-  efes_queue* q = u->q;
-  uint8_t st[kDevStateBytes];
-  DeviceGuard g(q->ctx->device);
-  hipError_t e = hipMemcpyAsync(st, q->d_states + (size_t)u->dslot * kDevStateBytes, sizeof st,
-                                hipMemcpyDeviceToHost, q->ctl);
-  if (e == hipSuccess) e = hipStreamSynchronize(q->ctl);
-  if (e != hipSuccess) return u->latched = EFES_ERR_DEVICE_FAULT;
+  const uint8_t* st = u->q->h_states + (size_t)u->dslot * kDevStateBytes;
   int32_t status;
   memcpy(&status, st + kOffStatus, 4);
   if (status != EFES_OK) return u->latched = status;
@@ -379,33 +375,23 @@ int efes_upload_state(efes_upload* u, efes_sha1_state* sha1, efes_crc32_state* c
 
 int efes_upload_sum(efes_upload* u, uint8_t out[24]) {
   if (!u || !out) return EFES_ERR_ARG;
-  int rc = wait_idle(u);
-  if (rc) return rc;
+  if (u->latched) return u->latched;
   efes_queue* q = u->q;
-  // A zero-length FINALIZE job on the control stream, kept in the upload's own device slot:
-  // Sum works on a copy (sha1.go:82-87), so the state stays as it is.
-  uint8_t* st = q->d_states + (size_t)u->dslot * kDevStateBytes;
-  efes_job job{};
-  job.data = nullptr;
-  job.length = 0;
-  job.sha1 = (u->hashes & EFES_HASH_SHA1) ? reinterpret_cast<efes_sha1_state*>(st) : nullptr;
-  job.crc32 = (u->hashes & EFES_HASH_CRC32) ? reinterpret_cast<efes_crc32_state*>(st + kOffCrc) : nullptr;
-  job.sum = st + kOffSum;
-  job.status = reinterpret_cast<int32_t*>(st + kOffStatus);
-  job.flags = EFES_JOB_FINALIZE;
-  uint8_t back[kOffStatus + 4 - kOffSum];
-  DeviceGuard g(q->ctx->device);
-  hipError_t e = hipMemcpyAsync(st + kOffJob, &job, sizeof job, hipMemcpyHostToDevice, q->ctl);
-  if (e == hipSuccess)
-    rc = efes_hash_submit_mode(q->ctx, reinterpret_cast<const efes_job*>(st + kOffJob), 1, q->ctl, EFES_MODE_DEEP);
-  if (e == hipSuccess && rc == EFES_OK) e = hipMemcpyAsync(back, st + kOffSum, sizeof back, hipMemcpyDeviceToHost, q->ctl);
-  if (e == hipSuccess) e = hipStreamSynchronize(q->ctl);
-  if (e != hipSuccess) return u->latched = EFES_ERR_DEVICE_FAULT;
-  if (rc != EFES_OK) return rc;
+  {
+    // A zero-length FINALIZE job through the dispatcher, after the upload's staged bytes.
+    std::unique_lock<std::mutex> lk(q->mu);
+    enqueue_current(u, lk);
+    q->pending.push_back(Pending{u, kNoChunk, 0});
+    ++u->inflight;
+    q->work.notify_one();
+    u->done.wait(lk, [&] { return u->inflight == 0; });
+  }
+  if (u->latched) return u->latched;
+  const uint8_t* st = q->h_states + (size_t)u->dslot * kDevStateBytes;
   int32_t status;
-  memcpy(&status, back + (kOffStatus - kOffSum), 4);
+  memcpy(&status, st + kOffStatus, 4);
   if (status != EFES_OK) return status;  // EFES_ERR_STATE: sha1.go:108 would panic
-  memcpy(out, back, 24);
+  memcpy(out, st + kOffSum, 24);
   return EFES_OK;
 }
 

@@ -1,0 +1,11 @@
+cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
+for rep in 1 2; do
+  for v in base new; do
+    for spec in "16 128 8192" "16 64 8192" "32 128 16384"; do
+      set -- $spec
+      if [ $v = base ]; then LP=$PWD/efes_amd/lib/ab_base; else LP=; fi
+      LD_LIBRARY_PATH=$LP timeout -k 10 300 ./tools/bench_uploads $1 $3 4194304 32768 $2 262144 > gpurun_out/up.json 2> gpurun_out/up.err || { echo "FAIL $v $spec"; tail -5 gpurun_out/up.err; exit 1; }
+      python3 -c "import json;d=json.load(open('gpurun_out/up.json'));print('$v T=$1 K=$2 U=$3', d['value'], 'GiB/s', d['seconds'], 's', d['all_sums_equal'], d['errors'])"
+    done
+  done
+done

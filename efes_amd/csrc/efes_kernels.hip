@@ -700,18 +700,10 @@ __device__ void group_bulk(const Tables& T, const PosTables& P, int lane, DeepMs
 #pragma unroll
   for (int k = 0; k < 16; ++k) A[k] = 0;
   if (live) load_block_le<kAligned16>(q + 64 * (uint64_t)i, A);
-  if constexpr (G <= 8) {  // two buffers, unrolled by two: no register copies of the prefetch
-    for (uint64_t st = 0; st < S; st += 2) {
-      super_step(A, B, st);
-      if (st + 1 >= S) break;
-      super_step(B, A, st + 1);
-    }
-  } else {  // (GROUP16/32: one buffer; the unrolled chain is already 16-32 blocks of code)
-    for (uint64_t st = 0; st < S; ++st) {
-      super_step(A, B, st);
-#pragma unroll
-      for (int k = 0; k < 16; ++k) A[k] = B[k];
-    }
+  for (uint64_t st = 0; st < S; st += 2) {  // two buffers, unrolled by two: no register copies of the prefetch
+    super_step(A, B, st);
+    if (st + 1 >= S) break;
+    super_step(B, A, st + 1);
   }
   wave_lds_sync();
   if (live && i == 0) {  // joint jobs only

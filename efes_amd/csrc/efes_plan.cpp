@@ -7,7 +7,7 @@
 //   shape                      latency of one job           SIMD work per job
 //   DEEP  (one wave per job)   422 x 4.1                    422 x 4.1
 //   GROUPn (64/n jobs / wave)  (410 + o_n/n) x 4.1          (410 n + o_n)/64 x 4.1
-//   (o_n = instructions per super-step besides the chain: 660 for n <= 8, 715 for n = 16, 32)
+//   (o_n = 665: instructions per super-step besides the chain, measured for n = 4..32)
 //   WIDE  (one lane per job)   740 x 5.1                    740/64 x 5.1 (/1.06 once SIMDs hold 2+ waves)
 // A DEEP/GROUP wave issues at ~4.1 cycles per instruction alone and gains almost nothing from
 // a second wave on its SIMD (1.06x), so where a long job's wave lands matters: the plan can
@@ -40,7 +40,7 @@ constexpr double kWideShare = 1.06; // WIDE throughput of a SIMD holding two wav
 constexpr double kClock = 2.36e9;   // Hz (GRBM_GUI_ACTIVE during DEEP), for est_seconds only
 constexpr int kWideLanes = 0;       // "shape" id of WIDE in the search
 
-double step_overhead(int g) { return g <= 8 ? 660.0 : 715.0; }  // double-buffered for g <= 8
+double step_overhead(int) { return 665.0; }
 double latency(int g) {  // cycles per block of one job
   if (g == kWideLanes) return 740.0 * kCpiWide;
   return (g == 64 ? 422.0 : 410.0 + step_overhead(g) / g) * kCpiDeep;

@@ -4,7 +4,7 @@
 // filereceiver.go:209) from ordinary pageable memory, then Sums each (filereceiver.go:99-100).
 // T x K concurrent uploads is what fills the GPU: each upload's SHA-1 is a serial chain.
 // Prints one JSON line.  Not part of the product library.
-//   tools/bench_uploads <threads> <uploads> <upload_bytes> <write_bytes> [open_per_thread] [chunk_bytes]
+//   tools/bench_uploads <threads> <uploads> <upload_bytes> <write_bytes> [open_per_thread] [chunk_bytes] [stagger]
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -20,7 +20,7 @@
 
 int main(int argc, char** argv) {
   if (argc < 5) {
-    fprintf(stderr, "usage: %s threads uploads upload_bytes write_bytes [chunk_bytes] [max_chunks]\n", argv[0]);
+    fprintf(stderr, "usage: %s threads uploads upload_bytes write_bytes [open_per_thread] [chunk_bytes] [stagger]\n", argv[0]);
     return 2;
   }
   const int T = atoi(argv[1]);
@@ -28,6 +28,7 @@ int main(int argc, char** argv) {
   const size_t S = strtoull(argv[3], nullptr, 10), W = strtoull(argv[4], nullptr, 10);
   const int K = argc > 5 ? atoi(argv[5]) : 64;
   const uint64_t chunk = argc > 6 ? strtoull(argv[6], nullptr, 10) : (256u << 10);
+  const int stagger = argc > 7 ? atoi(argv[7]) : 0;
   const uint32_t max_uploads = (uint32_t)(T * K);
   const uint32_t max_chunks = 4 * max_uploads + 64;
   efes_ctx* ctx = nullptr;
@@ -69,21 +70,33 @@ int main(int argc, char** argv) {
     th.emplace_back([&, t] {
       std::vector<long> mine;
       for (long u = t; u < U; u += T) mine.push_back(u);
-      for (size_t g = 0; g < mine.size(); g += (size_t)K) {  // K uploads in flight per thread
-        const size_t n = std::min(mine.size() - g, (size_t)K);
-        std::vector<efes_upload*> ups(n, nullptr);
-        for (auto& up : ups)
-          if (efes_upload_open(q, EFES_HASH_SHA1 | EFES_HASH_CRC32, nullptr, nullptr, &up)) { ++errs; return; }
-        for (size_t a = 0; a < S; a += W)
-          for (auto* up : ups)
-            if (efes_upload_write(up, src.data() + a, a + W <= S ? W : S - a)) { ++errs; return; }
+      // stagger 0: lockstep groups of K (open, write all, Sum all).  stagger 1: half-groups of
+      // K/2, each half's Sums taken after the NEXT half has been written, so a thread's Sum waits
+      // overlap its own writes (request goroutines at different phases, as on a real server).
+      const size_t grp = stagger ? std::max<size_t>(1, (size_t)K / 2) : (size_t)K;
+      std::vector<efes_upload*> pending;
+      auto sum_close = [&](std::vector<efes_upload*>& ups) {
         for (auto* up : ups) {
           uint8_t sum[24];
           if (efes_upload_sum(up, sum)) ++errs;
           else if (memcmp(first, sum, 24)) ++bad;
           efes_upload_close(up);
         }
+        ups.clear();
+      };
+      for (size_t g = 0; g < mine.size(); g += grp) {
+        const size_t n = std::min(mine.size() - g, grp);
+        std::vector<efes_upload*> ups(n, nullptr);
+        for (auto& up : ups)
+          if (efes_upload_open(q, EFES_HASH_SHA1 | EFES_HASH_CRC32, nullptr, nullptr, &up)) { ++errs; return; }
+        for (size_t a = 0; a < S; a += W)
+          for (auto* up : ups)
+            if (efes_upload_write(up, src.data() + a, a + W <= S ? W : S - a)) { ++errs; return; }
+        sum_close(pending);
+        pending = std::move(ups);
+        if (!stagger) sum_close(pending);
       }
+      sum_close(pending);
     });
   for (auto& x : th) x.join();
   const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -92,9 +105,9 @@ int main(int argc, char** argv) {
   char hex[49];
   for (int i = 0; i < 24; ++i) snprintf(hex + 2 * i, 3, "%02x", first[i]);
   printf("{\"workload\": \"uploads\", \"threads\": %d, \"uploads\": %ld, \"upload_bytes\": %zu, \"write_bytes\": %zu, "
-         "\"open_per_thread\": %d, \"chunk_bytes\": %llu, \"max_chunks\": %u, \"seconds\": %.4f, \"value\": %.3f, \"unit\": \"GiB/s\", "
+         "\"open_per_thread\": %d, \"stagger\": %d, \"chunk_bytes\": %llu, \"max_chunks\": %u, \"seconds\": %.4f, \"value\": %.3f, \"unit\": \"GiB/s\", "
          "\"sum_sha1_crc32\": \"%s\", \"all_sums_equal\": %s, \"errors\": %d}\n",
-         T, U, S, W, K, (unsigned long long)chunk, max_chunks, secs, (double)U * S / secs / (1u << 30), hex,
+         T, U, S, W, K, stagger, (unsigned long long)chunk, max_chunks, secs, (double)U * S / secs / (1u << 30), hex,
          bad ? "false" : "true", errs.load());
   return errs || bad ? 1 : 0;
 }

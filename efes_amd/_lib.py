@@ -28,6 +28,7 @@ EFES_ERR_DEVICE_FAULT = -7
 
 EFES_JOB_FINALIZE = 0x1
 EFES_JOB_INIT = 0x2
+EFES_JOB_SUM_ONLY = 0x4
 EFES_HASH_SHA1, EFES_HASH_CRC32 = 0x1, 0x2
 EFES_HOST_ZERO_COPY = (1 << 64) - 1
 MODE_AUTO, MODE_DEEP, MODE_WIDE = 0, 1, 2

@@ -9,7 +9,7 @@ from __future__ import annotations
 
 import numpy as np
 
-from ._lib import EFES_JOB_FINALIZE, EFES_JOB_INIT, JOB_DTYPE, MODE_AUTO, SHA1_STATE_DTYPE
+from ._lib import EFES_JOB_FINALIZE, EFES_JOB_INIT, EFES_JOB_SUM_ONLY, JOB_DTYPE, MODE_AUTO, SHA1_STATE_DTYPE
 from .hashing import Context, default_context
 
 MODE_PLAN = -1  # run(): efes_plan_batch + efes_hash_submit_plan instead of one fixed kernel shape
@@ -27,14 +27,15 @@ def fresh_states(n: int) -> np.ndarray:
 class DeviceBatch:
     """Jobs j = 0..N-1: Write(data[offsets[j] : offsets[j]+lengths[j]]) into state j (+ Sum).
 
-    Kernels run on torch's current stream when it is not the null stream; a null-stream
-    handle (0) selects the context's own stream (efes_hash.h), and run() synchronises the
-    whole device either way.
+    Kernels run on torch's current stream.  When that is the null stream (handle 0, which
+    efes_hash.h maps to the context's own non-blocking stream), submit() orders the context
+    stream after the work torch queued so far and torch's stream after the launch, so
+    reset() / result reads on torch's stream stay ordered with the kernels either way.
     """
 
     def __init__(self, data_ptr: int, offsets, lengths, *, sha1: bool = True, crc32: bool = True,
                  finalize: bool = True, fresh: bool = False, states: np.ndarray | None = None, crcs: np.ndarray | None = None,
-                 ctx: Context | None = None, device: str = "cuda:0"):
+                 ctx: Context | None = None, device: str = "cuda:0", sum_only: bool = False):
         import torch
 
         self.ctx = ctx or default_context(int(device.split(":")[1]) if ":" in device else 0)
@@ -64,6 +65,9 @@ class DeviceBatch:
             jobs["flags"] |= EFES_JOB_FINALIZE
         if fresh:  # new chunks: start from NewSha1()/NewCRC32IEEE(), in-states are not read
             jobs["flags"] |= EFES_JOB_INIT
+        if sum_only:  # Sum of the in-states on a copy (sha1.go:82-87): states are not written
+            assert finalize and not lengths.any(), "sum_only jobs are zero-length FINALIZE jobs"
+            jobs["flags"] |= EFES_JOB_SUM_ONLY
         jobs["status"] = np.uint64(self.status.data_ptr()) + np.arange(n, dtype=np.uint64) * np.uint64(4)
         self.jobs_host = jobs
         self.jobs = torch.from_numpy(jobs.view(np.uint8).copy()).to(device)
@@ -78,11 +82,26 @@ class DeviceBatch:
         self.crcs.copy_(self._init_crcs_dev)
 
     def submit(self, mode: int = MODE_AUTO) -> None:
-        """Enqueue all jobs on torch's current stream (ordered after the data it wrote)."""
+        """Enqueue all jobs, ordered after the work on torch's current stream (data writes,
+        reset()) and before the work queued there afterwards (result copies)."""
+        cur = self.torch.cuda.current_stream(self.device)
+        if cur.cuda_stream:
+            self._launch(mode, cur.cuda_stream)
+            return
+        # Null stream: the library launches on the context's non-blocking stream, which the
+        # null stream does not order against; join the two both ways with events.
+        ctx_stream = self.torch.cuda.ExternalStream(self.ctx.stream, device=self.device)
+        ctx_stream.wait_stream(cur)
+        self._launch(mode, ctx_stream.cuda_stream)
+        cur.wait_stream(ctx_stream)
+
+    def _launch(self, mode: int, stream: int) -> None:
         if mode == MODE_PLAN:
-            self.submit_planned()
+            if not hasattr(self, "plan"):
+                self.make_plan()
+            self.ctx.submit_plan(self.jobs_planned.data_ptr(), self.plan, stream)
         else:
-            self.ctx.submit(self.jobs.data_ptr(), self.n, self.stream(), mode)
+            self.ctx.submit(self.jobs.data_ptr(), self.n, stream, mode)
 
     def run(self, mode: int = MODE_AUTO) -> None:
         self.submit(mode)
@@ -95,11 +114,8 @@ class DeviceBatch:
         self.torch.cuda.synchronize(self.device)
 
     def submit_planned(self) -> None:
-        """The planned launch (DEEP/grouped part concurrent with the WIDE part) on torch's current stream."""
-        if not hasattr(self, "plan"):
-            self.make_plan()
-        self.ctx.submit_plan(self.jobs_planned.data_ptr(), self.plan, self.stream())
-
+        """The planned launch (DEEP/grouped part concurrent with the WIDE part), ordered like submit()."""
+        self.submit(MODE_PLAN)
 
     # ---- results (host copies)
     def status_host(self) -> np.ndarray:

@@ -373,8 +373,9 @@ __device__ void deep_rest(const Tables& T, int lane, const DeepJob& J, uint8_t* 
     }
   }
 
-  // ---- write back
-  if (do_sha) {
+  // ---- write back (a Sum-only job leaves the states alone: Go's Sum works on a copy)
+  const bool keep = (J.flags & EFES_JOB_SUM_ONLY) != 0;
+  if (do_sha && !keep) {
     if (lane < 5) {
       uint32_t v = h[0];
 #pragma unroll
@@ -387,7 +388,7 @@ __device__ void deep_rest(const Tables& T, int lane, const DeepJob& J, uint8_t* 
       J.st->len = len;
     }
   }
-  if (do_crc && lane == 0) J.cs->crc = ~crc_raw;
+  if (do_crc && !keep && lane == 0) J.cs->crc = ~crc_raw;
   if (fin && J.sum && lane < 6) {
     uint32_t v;
     if (lane < 5) {
@@ -1065,9 +1066,10 @@ __global__ __launch_bounds__(64 * kWideWaves, 2) void wide_kernel(const efes_job
     }
   }
 
-  // ---- write back
+  // ---- write back (a Sum-only job leaves the states alone: Go's Sum works on a copy)
+  const bool keep = (jb.flags & EFES_JOB_SUM_ONLY) != 0;
   if (go) {
-    if (do_sha) {
+    if (do_sha && !keep) {
 #pragma unroll
       for (int k = 0; k < 5; ++k) st->h[k] = h[k];
 #pragma unroll
@@ -1077,7 +1079,7 @@ __global__ __launch_bounds__(64 * kWideWaves, 2) void wide_kernel(const efes_job
       st->nx = nx_new;
       st->len = len;
     }
-    if (do_crc) cs->crc = ~crc_raw;
+    if (do_crc && !keep) cs->crc = ~crc_raw;
     if (fin && jb.sum) {
 #pragma unroll
       for (int k = 0; k < 5; ++k) reinterpret_cast<uint32_t*>(jb.sum)[k] = bswap(status == EFES_OK ? dig[k] : 0u);

@@ -151,7 +151,7 @@ void efes_queue::run() {
     for (size_t i = 0; i < b.items.size(); ++i) {
       const Pending& p = b.items[i];
       uint8_t* st = z_states + (size_t)p.u->dslot * kDevStateBytes;
-      const bool sum = p.slot == kNoChunk;  // Sum: works on a copy (sha1.go:82-87), state unchanged
+      const bool sum = p.slot == kNoChunk;  // Sum: works on a copy (sha1.go:82-87), state unchanged (SUM_ONLY)
       efes_job& j = hj[i];
       j.data = sum ? nullptr : z_slab + (size_t)p.slot * chunk;
       j.length = sum ? 0 : p.len;
@@ -159,7 +159,7 @@ void efes_queue::run() {
       j.crc32 = (p.u->hashes & EFES_HASH_CRC32) ? reinterpret_cast<efes_crc32_state*>(st + kOffCrc) : nullptr;
       j.sum = sum ? st + kOffSum : nullptr;
       j.status = reinterpret_cast<int32_t*>(st + kOffStatus);
-      j.flags = sum ? EFES_JOB_FINALIZE : 0u;
+      j.flags = sum ? EFES_JOB_FINALIZE | EFES_JOB_SUM_ONLY : 0u;
       j._reserved = 0;
     }
     lk.unlock();  // callers keep staging while this batch is copied and launched
@@ -387,10 +387,17 @@ int efes_upload_sum(efes_upload* u, uint8_t out[24]) {
     u->done.wait(lk, [&] { return u->inflight == 0; });
   }
   if (u->latched) return u->latched;
-  const uint8_t* st = q->h_states + (size_t)u->dslot * kDevStateBytes;
+  uint8_t* st = q->h_states + (size_t)u->dslot * kDevStateBytes;
   int32_t status;
   memcpy(&status, st + kOffStatus, 4);
-  if (status != EFES_OK) return status;  // EFES_ERR_STATE: sha1.go:108 would panic
+  if (status != EFES_OK) {
+    // EFES_ERR_STATE: checkSum panics (sha1.go:108) on a copy, so the digest itself stays
+    // usable; clear the slot's status (no job of this upload is in flight) so a later
+    // efes_upload_state / MarshalText does not latch this Sum's failure.
+    const int32_t ok = EFES_OK;
+    memcpy(st + kOffStatus, &ok, 4);
+    return status;
+  }
   memcpy(out, st + kOffSum, 24);
   return EFES_OK;
 }

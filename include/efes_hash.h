@@ -81,6 +81,9 @@ void* efes_ctx_stream(efes_ctx* ctx);
 #define EFES_JOB_FINALIZE 0x1u /* also write Sum of the post-Write state to `sum` */
 #define EFES_JOB_INIT 0x2u     /* start from NewSha1() / NewCRC32IEEE() (sha1.go:48-52, crc32.go:68):
                                   the in-states are not read, only written (a fresh chunk) */
+#define EFES_JOB_SUM_ONLY 0x4u /* with EFES_JOB_FINALIZE and length 0: Sum of the in-state on a copy
+                                  (sha1.go:82-87 `d0 := *d`): the states are read, never written, so
+                                  a pending full tail (nx == 64) stays pending as in Go */
 
 /* One `Write(p)` (+ optional Sum) of len(p) = length bytes at device address `data`.
  * sha1 / crc32: device states updated in place; either may be NULL to skip that hash

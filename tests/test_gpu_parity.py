@@ -702,6 +702,76 @@ def test_streaming_full_tail_empty_write(env, oracle):
     assert d.sum().hex() == o.hexdigest()
 
 
+def test_streaming_sum_keeps_full_tail_pending(env, oracle):
+    """Sum right after UnmarshalText of an nx == 64 state works on a copy (sha1.go:82-87): the
+    pending block stays pending, so MarshalText is unchanged until the next Write."""
+    h = env["hashing"]
+    o = oracle.Sha1()
+    o.st.x[:] = bytes(range(100, 164))
+    o.st.nx, o.st.len = 64, 64
+    text = o.marshal_text()
+    d = h.new_sha1()
+    d.unmarshal_text(text.encode())
+    assert d.sum().hex() == o.hexdigest()
+    assert d.marshal_text().decode() == o.marshal_text() == text
+    d.write(b"more")
+    o.write(b"more")
+    assert d.marshal_text().decode() == o.marshal_text()
+    assert d.sum().hex() == o.hexdigest()
+
+
+def test_streaming_failed_sum_leaves_digest_usable(env, oracle):
+    """A Sum that Go would panic on (checkSum, sha1.go:107-109) runs on a copy: MarshalText and
+    later Writes still behave as Go's."""
+    h = env["hashing"]
+    efes = env["efes"]
+    o = oracle.Sha1()
+    o.st.x[:3] = b"\x01\x02\x03"
+    o.st.nx, o.st.len = 3, 0  # nx inconsistent with len: the padding never lands on a block edge
+    text = o.marshal_text()
+    d = h.new_sha1()
+    d.unmarshal_text(text.encode())
+    with pytest.raises(efes.EfesError) as e:
+        d.sum()
+    assert e.value.code == efes.EFES_ERR_STATE
+    assert d.marshal_text().decode() == text
+    d.write(b"y" * 200)
+    o.write(b"y" * 200)
+    assert d.marshal_text().decode() == o.marshal_text()
+    with pytest.raises(efes.EfesError):  # len is still inconsistent with nx
+        d.sum()
+    assert d.marshal_text().decode() == o.marshal_text()
+
+
+@pytest.mark.parametrize("mode", MODE_IDS)
+def test_sum_only_jobs_leave_states(env, oracle, mode):
+    """EFES_JOB_SUM_ONLY: the Sum of each in-state, states never written back (sha1.go:82-87)."""
+    rng = random.Random(23)
+    n = 40
+    states, crcs = midstream_states(oracle, env, n, rng)
+    states[0]["x"] = np.arange(64, dtype=np.uint8); states[0]["nx"] = 64; states[0]["len"] = 64
+    states[1]["nx"] = 5; states[1]["len"] = 0  # Go panics in checkSum
+    buf = device_buffer(env, np.zeros(64, np.uint8))
+    b = env["DeviceBatch"](buf.data_ptr(), [0] * n, [0] * n, states=states, crcs=crcs, sum_only=True,
+                           ctx=env["ctx"])
+    b.run(_modes(env)[mode])
+    status, st, crc, sums = b.status_host(), b.states_host(), b.crc_sum(), b.sums_host()
+    for i in range(n):
+        assert bytes(st[i].tobytes()) == bytes(states[i].tobytes()), (mode, i)
+        assert int(crc[i]) == int(crcs[i]), (mode, i)
+        o = oracle.Sha1(reset=False)
+        o.st.h[:] = [int(v) for v in states[i]["h"]]
+        o.st.x[:] = bytes(states[i]["x"])
+        o.st.nx, o.st.len = int(states[i]["nx"]), int(states[i]["len"])
+        src, digest = o.sum()
+        if src:
+            assert status[i] == env["efes"].EFES_ERR_STATE, (mode, i)
+            continue
+        assert status[i] == 0, (mode, i)
+        assert bytes(sums[i][:20]) == digest, (mode, i)
+        assert bytes(sums[i][20:]) == int(crcs[i]).to_bytes(4, "big"), (mode, i)
+
+
 def test_host_ingest_zero_copy(env, oracle):
     """EFES_HOST_ZERO_COPY: the kernel reads pinned host chunks in place; pageable data is refused."""
     from efes_amd._lib import EFES_HOST_ZERO_COPY

@@ -74,7 +74,16 @@ int main(int argc, char** argv) {
       // K/2, each half's Sums taken after the NEXT half has been written, so a thread's Sum waits
       // overlap its own writes (request goroutines at different phases, as on a real server).
       const size_t grp = stagger ? std::max<size_t>(1, (size_t)K / 2) : (size_t)K;
-      std::vector<efes_upload*> pending;
+      std::vector<efes_upload*> pending, ups;
+      // Error exit: close every upload this thread still holds (efes_queue_destroy requires it).
+      auto fail = [&] {
+        ++errs;
+        for (auto* up : ups)
+          if (up) efes_upload_close(up);
+        for (auto* up : pending) efes_upload_close(up);
+        ups.clear();
+        pending.clear();
+      };
       auto sum_close = [&](std::vector<efes_upload*>& ups) {
         for (auto* up : ups) {
           uint8_t sum[24];
@@ -86,12 +95,12 @@ int main(int argc, char** argv) {
       };
       for (size_t g = 0; g < mine.size(); g += grp) {
         const size_t n = std::min(mine.size() - g, grp);
-        std::vector<efes_upload*> ups(n, nullptr);
+        ups.assign(n, nullptr);
         for (auto& up : ups)
-          if (efes_upload_open(q, EFES_HASH_SHA1 | EFES_HASH_CRC32, nullptr, nullptr, &up)) { ++errs; return; }
+          if (efes_upload_open(q, EFES_HASH_SHA1 | EFES_HASH_CRC32, nullptr, nullptr, &up)) return fail();
         for (size_t a = 0; a < S; a += W)
           for (auto* up : ups)
-            if (efes_upload_write(up, src.data() + a, a + W <= S ? W : S - a)) { ++errs; return; }
+            if (efes_upload_write(up, src.data() + a, a + W <= S ? W : S - a)) return fail();
         sum_close(pending);
         pending = std::move(ups);
         if (!stagger) sum_close(pending);

@@ -1,6 +1,6 @@
 # A/B of library builds over several bench workloads (same device, interleaved):
 #   LIBS="a.so b.so" REPS=2 bash tools/gpu_ab_multi.sh "<bench args 1>" "<bench args 2>" ...
-cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
+cd "${GRAFT_REPO_ROOT:?}" || exit 1; mkdir -p gpurun_out
 for rep in $(seq 1 ${REPS:-2}); do
   for args in "$@"; do
     for lib in $LIBS; do

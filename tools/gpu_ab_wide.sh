@@ -1,6 +1,6 @@
 # A/B of library builds on WIDE-heavy workloads (same device, interleaved):
 #   LIBS="a.so b.so" bash tools/gpu_ab_wide.sh
-cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
+cd "${GRAFT_REPO_ROOT:?}" || exit 1; mkdir -p gpurun_out
 for rep in 1 2; do
   for lib in $LIBS; do
     for args in "--chunks 8192 --mode wide --steps 3 --warmup 1" "--workload ingest --ingest-scale 0.4 --ingest-batch 131072 --mode wide --warmup 1" "--chunks 65536 --chunk-bytes 65536 --mode wide --steps 5 --warmup 1"; do

@@ -1,5 +1,5 @@
 # PMC passes (each its own run, kernel-trace only): bash tools/gpu_pmc.sh <tag> <bench args...>
-cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out; export TMPDIR=/tmp
+cd "${GRAFT_REPO_ROOT:?}" || exit 1; mkdir -p gpurun_out; export TMPDIR=/tmp
 TAG=$1; shift
 timeout -k 10 120 rocprofv3 -L > gpurun_out/rocprof_counters.txt 2>&1 || true
 i=0

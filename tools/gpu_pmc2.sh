@@ -1,5 +1,5 @@
 # Extra PMC passes (instruction cache, LDS/scalar activity): bash tools/gpu_pmc2.sh <tag> <bench args...>
-cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out; export TMPDIR=/tmp
+cd "${GRAFT_REPO_ROOT:?}" || exit 1; mkdir -p gpurun_out; export TMPDIR=/tmp
 TAG=$1; shift
 i=10
 for set in "SQC_ICACHE_HITS SQC_ICACHE_MISSES" "SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VMEM SQ_IFETCH SQ_INST_CYCLES_SALU SQ_WAVE_CYCLES SQ_WAIT_ANY"; do

@@ -17,7 +17,7 @@ for s in $STEPS; do
   case $s in
     smoke) timeout -k 10 300 python __graft_entry__.py smoke > $OUT/smoke_$TAG.log 2>&1; rc=$?
            echo "smoke rc=$rc"; tail -3 $OUT/smoke_$TAG.log; fatal $rc $OUT/smoke_$TAG.log ;;
-    tests) timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider > $OUT/gpu_tests_$TAG.log 2>&1; rc=$?
+    tests) timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider > $OUT/gpu_tests_$TAG.log 2>&1; rc=$?
            echo "tests rc=$rc"; tail -15 $OUT/gpu_tests_$TAG.log; fatal $rc $OUT/gpu_tests_$TAG.log ;;
     bench) timeout -k 10 400 python bench.py > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err; rc=$?
            echo "bench rc=$rc"; cat $OUT/bench_$TAG.json; tail -5 $OUT/bench_$TAG.err; fatal $rc $OUT/bench_$TAG.err ;;

@@ -1,6 +1,6 @@
 # Run the uploads harness under ThreadSanitizer (build first: bash tools/tsan_build.sh):
 # concurrent writers, the dispatcher thread and the per-upload sync points on the real GPU.
-cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
+cd "${GRAFT_REPO_ROOT:?}" || exit 1; mkdir -p gpurun_out
 export TSAN_OPTIONS="halt_on_error=0 report_signal_unsafe=0 history_size=4 log_path=gpurun_out/tsan suppressions=$PWD/tools/tsan.supp"
 for spec in "8 512 1048576 32768 32 262144" "16 256 262144 4096 16 65536"; do
   timeout -k 10 300 ./tools/bench_uploads_tsan $spec > gpurun_out/tsan_run.json 2> gpurun_out/tsan_run.err

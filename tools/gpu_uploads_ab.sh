@@ -1,5 +1,5 @@
 # A/B of the upload dispatcher's kernel shape: default lib vs efes_amd/lib/ab_deep (DEEP forced).
-cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
+cd "${GRAFT_REPO_ROOT:?}" || exit 1; mkdir -p gpurun_out
 for rep in 1 2; do
   for v in default ab_deep; do
     for spec in "16 64 262144" "16 128 262144" "32 128 262144"; do

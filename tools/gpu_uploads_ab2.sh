@@ -1,4 +1,4 @@
-cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
+cd "${GRAFT_REPO_ROOT:?}" || exit 1; mkdir -p gpurun_out
 for rep in 1 2; do
   for v in base new; do
     for spec in "16 128 8192" "16 64 8192" "32 128 16384"; do

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Uploads harness: lockstep request groups (stagger 0) vs staggered half-groups (stagger 1),
 # interleaved on one device.  Usage (GPU box, repo root): bash tools/gpu_uploads_stagger.sh
-cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out/uploads_stagger
+cd "${GRAFT_REPO_ROOT:?}" || exit 1; mkdir -p gpurun_out/uploads_stagger
 for rep in 1 2; do
   for spec in "16 128 8192" "32 128 16384" "32 256 16384"; do
     for st in 0 1; do

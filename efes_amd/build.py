@@ -61,6 +61,18 @@ def build_tools() -> list[str]:
     return out
 
 
+def build_consumer_test() -> str:
+    """tests/c/efes_consumer_test: a C consumer of the ABI checked against the oracle (test infrastructure)."""
+    src = os.path.join(ROOT, "tests", "c", "efes_consumer_test.c")
+    exe = os.path.join(ROOT, "tests", "c", "efes_consumer_test")
+    oracle_lib = os.path.join(ROOT, "oracle", "liboracle.so")
+    if os.path.exists(src) and _stale(exe, [src, LIB, oracle_lib, os.path.join(ROOT, "include", "efes_hash.h")]):
+        subprocess.run(["gcc", "-O2", "-std=c11", "-Wall", "-Wextra", "-pthread", src, "-o", exe,
+                        "-L", LIB_DIR, "-lefeshash", "-L", os.path.join(ROOT, "oracle"), "-loracle",
+                        "-Wl,-rpath,$ORIGIN/../../efes_amd/lib", "-Wl,-rpath,$ORIGIN/../../oracle"], check=True)
+    return exe
+
+
 def build_oracle() -> str:
     """The CPU checker (test infrastructure; never linked into the product)."""
     subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
@@ -71,3 +83,4 @@ if __name__ == "__main__":
     print(build_lib(force="--force" in sys.argv, verbose=True))
     print(build_tools())
     print(build_oracle())
+    print(build_consumer_test())

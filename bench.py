@@ -43,7 +43,7 @@ def parse_args(argv=None):
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--chunks", type=int, default=1024, help="chunks per GPU")
     p.add_argument("--chunk-bytes", type=int, default=4 << 20)
-    p.add_argument("--mode", choices=["auto", "deep", "wide", "plan", "group4", "group8", "group16", "group32"],
+    p.add_argument("--mode", choices=["auto", "deep", "wide", "plan", "group4", "group8", "group16", "group32", "fed4"],
                    default="auto", help="auto: AUTO for chunks4m/ingest, plan (efes_plan_batch) for mixed")
     p.add_argument("--workload", choices=["chunks4m", "mixed", "ingest", "uploads"], default="chunks4m",
                    help="chunks4m = BASELINE configs[1]/[2] (the metric); mixed = configs[3]; ingest = configs[4]")
@@ -372,7 +372,7 @@ def mixed_leg(args, rank: int, world: int, ctx, device: str, stream):
 
     import torch
 
-    from efes_amd._lib import MODE_DEEP, MODE_GROUP, MODE_WIDE
+    from efes_amd._lib import MODE_DEEP, MODE_FED4, MODE_GROUP, MODE_WIDE
     from efes_amd.batch import MODE_PLAN
 
     a = _ap.Namespace(**vars(args))
@@ -383,7 +383,7 @@ def mixed_leg(args, rank: int, world: int, ctx, device: str, stream):
             b.make_plan()
         wall, kernel_ms = run_timed(batches, len(batches), 1, MODE_PLAN, device, stream, None)
     total = sum(step_bytes)
-    names = {MODE_DEEP: "deep_kernel", MODE_WIDE: "wide_kernel"}
+    names = {MODE_DEEP: "deep_kernel", MODE_WIDE: "wide_kernel", MODE_FED4: "fed_kernel"}
     names.update({v: f"group_kernel<{g}>" for g, v in MODE_GROUP.items()})
     parts = [{"jobs": j, "kernel": names[m], "exclusive_cus": x} for j, m, x in batches[0].plan.parts()]
     achieved = total / len(batches) / (kernel_ms * 1e-3) / 1e9
@@ -401,7 +401,7 @@ def main(argv=None):
     import torch
 
     from efes_amd import MODE_AUTO, MODE_DEEP, MODE_WIDE
-    from efes_amd._lib import MODE_GROUP, lib
+    from efes_amd._lib import MODE_FED4, MODE_GROUP, lib
     from efes_amd.batch import MODE_PLAN
     from efes_amd.hashing import default_context
     from efes_amd.shard import env_rank, max_over_ranks
@@ -425,6 +425,7 @@ def main(argv=None):
     stream = torch.cuda.Stream(device=device)
     modes = {"auto": MODE_AUTO, "deep": MODE_DEEP, "wide": MODE_WIDE, "plan": MODE_PLAN}
     modes.update({f"group{g}": v for g, v in MODE_GROUP.items()})
+    modes["fed4"] = MODE_FED4
     mode = modes["plan" if args.mode == "auto" and args.workload == "mixed" else args.mode]
 
     if args.workload == "uploads":
@@ -448,13 +449,14 @@ def main(argv=None):
     value = world * bytes_timed / wall / GiB
     njobs = batches[0].n
     launched = lib().efes_auto_mode(ctx.handle, njobs) if mode == MODE_AUTO else mode
-    kernel_name = {MODE_DEEP: "deep_kernel", MODE_WIDE: "wide_kernel"}.get(launched, "group_kernel")
+    kernel_name = {MODE_DEEP: "deep_kernel", MODE_WIDE: "wide_kernel", MODE_FED4: "fed_kernel"}.get(launched,
+                                                                                                  "group_kernel")
     if launched in MODE_GROUP.values():
         kernel_name = f"group_kernel<{ {v: g for g, v in MODE_GROUP.items()}[launched] }>"
     plan = None
     if mode == MODE_PLAN:
         p0 = batches[0].plan
-        names = {MODE_DEEP: "deep_kernel", MODE_WIDE: "wide_kernel"}
+        names = {MODE_DEEP: "deep_kernel", MODE_WIDE: "wide_kernel", MODE_FED4: "fed_kernel"}
         names.update({v: f"group_kernel<{g}>" for g, v in MODE_GROUP.items()})
         plan = {"parts": [{"jobs": j, "kernel": names[m], "exclusive_cus": x} for j, m, x in p0.parts()],
                 "model_seconds": round(p0.est_seconds, 4)}

@@ -33,6 +33,7 @@ EFES_HASH_SHA1, EFES_HASH_CRC32 = 0x1, 0x2
 EFES_HOST_ZERO_COPY = (1 << 64) - 1
 MODE_AUTO, MODE_DEEP, MODE_WIDE = 0, 1, 2
 MODE_GROUP = {4: 3, 8: 4, 16: 5, 32: 6}  # grouped DEEP: lanes per job -> EFES_MODE_GROUPn
+MODE_FED4 = 7  # grouped DEEP fed by a producer wave on another SIMD (EFES_MODE_FED4)
 
 
 class HostStats(ctypes.Structure):

@@ -53,6 +53,9 @@ hipError_t launch_wide(const efes_job* jobs, uint32_t njobs, const Tables* tabs,
 // workgroup reserves all LDS of its CU, so no other workgroup shares the CU's SIMDs.
 hipError_t launch_group(const efes_job* jobs, uint32_t njobs, int G, const Tables* tabs, hipStream_t s,
                         bool exclusive = false);
+// Grouped DEEP fed by a producer wave on another SIMD (EFES_MODE_FED4): 48 jobs per workgroup,
+// which always owns its CU.
+hipError_t launch_fed(const efes_job* jobs, uint32_t njobs, const Tables* tabs, hipStream_t s);
 hipError_t launch_fill(void* dst, size_t bytes, uint64_t seed, hipStream_t s);
 
 // Kernel shape for jobs whose bytes are read over PCIe in place (pinned, device-mapped host

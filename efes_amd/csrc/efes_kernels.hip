@@ -306,6 +306,9 @@ __device__ DeepMsg deep_head(const Tables& T, int lane, const DeepJob& J, uint8_
 
 // The rest of one Write after the head: bulk blocks [M.done, M.nbulk) (sha1.go:70-74), the
 // tail (:75-77), Sum (:82-120) on a copy, and the write-back of state, crc, sum and status.
+// kBulk = false: the caller has hashed every bulk block (M.done == M.nbulk) and T may hold only
+// the slicing-by-8 table (FED kernel).
+template <bool kBulk = true>
 __device__ void deep_rest(const Tables& T, int lane, const DeepJob& J, uint8_t* xs, uint8_t* fb, DeepMsg M) {
   const bool do_sha = J.st != nullptr, do_crc = J.cs != nullptr;
   const bool fin = (J.flags & EFES_JOB_FINALIZE) != 0;
@@ -319,7 +322,7 @@ __device__ void deep_rest(const Tables& T, int lane, const DeepJob& J, uint8_t* 
   uint64_t len = do_sha && !(J.flags & EFES_JOB_INIT) ? uniform64(J.st->len) : 0;
 
   // ---- bulk whole blocks not hashed yet (sha1.go:70-74)
-  if (nbulk > M.done) {
+  if (kBulk && nbulk > M.done) {
     const uint8_t* q = M.q + 64 * M.done;
     if ((reinterpret_cast<uintptr_t>(q) & 15) == 0)
       deep_bulk<true>(T, lane, q, nbulk - M.done, do_sha, do_crc, h, crc_raw);
@@ -794,6 +797,362 @@ __global__ __launch_bounds__(64 * kDeepWaves, 1) void group_kernel(const efes_jo
   }
 }
 
+// ================================================================== FED kernel: grouped DEEP fed from other SIMDs
+// The grouped kernel's chain wave spends (410 G + ~665) instructions per super-step: the chain
+// plus the loads, CRC and W+K expansion of its 64 blocks, all on one SIMD, so a job's latency is
+// 410 + 665/G per block (GROUP4: 577).  Here a workgroup owns its CU (its LDS fills the CU) and
+// splits that work across the CU's four SIMDs (one wave each): C chain waves holding 64/G jobs of
+// G lanes each, and 4 - C producer waves.  Per super-step of a chain wave, its producer loads the
+// 64 blocks (G consecutive blocks of each job, coalesced, prefetched a super-step ahead), computes
+// their CRC-32 (position tables: 64 independent lookups per block, the G-lane shift tree, the fold
+// into each job's running CRC) and the W+K expansion, and hands W+K over through LDS as the DEEP
+// kernel does (20 ds_write_b128 per lane).  The chain wave copies its lane's 80 words out
+// (20 ds_read_b128) and runs G chains: 410 + ~50/G instructions per block, DEEP's per-job latency.
+// A producer serves its chain waves round-robin, polling their slots (measured: one item, i.e.
+// one chain super-step, costs the producer ~3.9k cycles against the chain's ~6.9k at G = 4).
+// Heads, left-over blocks (< G per job), tails and Sums run on the chain waves.
+//   FED4 = <G 4, 2 chain waves + 2 producers>: 32 jobs per CU.
+template <int G, int C>
+struct FedCfg {
+  static constexpr int kJobs = 64 / G;  // jobs per chain wave
+  static constexpr int kProducers = 4 - C;
+  static constexpr int kLG = G == 4 ? 2 : G == 8 ? 3 : 0;
+  static_assert(kLG > 0 && C >= 1 && C <= 3, "G in {4, 8}, 1..3 chain waves");
+};
+
+struct FedSlot {
+  uint4 wk[20][64];   // [word quad][lane], as PipeSlot
+  uint64_t S;         // super-steps of the posted round
+  uint32_t flags;     // bit 0: some joint job hashes SHA-1, bit 1: CRC-32, bit 2: all blocks 16-B aligned
+  uint32_t req;       // chain -> producer: rounds posted
+  uint32_t fin;       // chain -> producer: no more rounds
+  uint32_t ready;     // producer -> chain: super-steps whose W+K is in wk (running count)
+  uint32_t taken;     // chain -> producer: super-steps copied out of wk
+  uint32_t crc_done;  // producer -> chain: rounds whose CRCs are back in the job's DeepMsg
+};
+
+// The LDS copy of the tables: the slicing-by-8 table and shift levels 0..3 (the tree and fold for
+// G <= 8) -- a prefix of Tables, so deep_head / deep_rest<false> can take it as one -- and the
+// position tables for the producer's CRC.
+constexpr int kFedShift = 4;
+struct FedTables {
+  uint32_t slice8[8][256];
+  uint32_t shift[kFedShift][4][256];
+};
+static_assert(offsetof(Tables, shift) == offsetof(FedTables, shift), "FedTables is a prefix of Tables");
+
+template <int G, int C>
+struct FedLDS {
+  static constexpr int kJobs = FedCfg<G, C>::kJobs;
+  FedTables tab;                // 24 KiB
+  PosTables pos;                // 64 KiB
+  FedSlot slot[C];              // 20 KiB each
+  DeepMsg msg[C][kJobs];
+  uint8_t xs[C][kJobs][64];
+  uint8_t fin[C][192];
+};
+
+#ifdef EFES_FED_STATS
+// Diagnostic build only (tools/fed_stats.py): per-wave cycle counts of workgroup 0.
+__device__ unsigned long long g_fed_stats[16];
+#define FED_STAT(...) __VA_ARGS__
+#else
+#define FED_STAT(...)
+#endif
+
+// Counters run modulo 2^32: "a has reached b".
+__device__ __forceinline__ bool reached(uint32_t a, uint32_t b) { return (int32_t)(a - b) >= 0; }
+__device__ __forceinline__ uint32_t lds_acq32(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// Release store issued HERE: the scheduling barrier keeps the compiler from sinking it below the
+// (fully unrolled) work that follows, which would hold the other side up for that long.
+__device__ __forceinline__ void lds_rel32(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// One lane's block of a fed super-step (zeros for a lane whose job sits the round out).
+__device__ __forceinline__ void fed_load(const uint8_t* src, bool live, bool a16, uint32_t (&le)[16]) {
+#pragma unroll
+  for (int k = 0; k < 16; ++k) le[k] = 0;
+  if (live) {
+    if (a16) load_block_le<true>(src, le);
+    else load_block_le<false>(src, le);
+  }
+}
+
+// Producer-side state of one chain wave's current round.
+struct FedFeed {
+  const uint8_t* q;  // this lane's job: first byte of the round (M.q + 64 * (M.done + i))
+  uint64_t S, st;    // super-steps of the round, produced so far
+  uint32_t gstep;    // super-steps produced for this chain wave, all rounds
+  uint32_t round;    // rounds served
+  uint32_t crc;      // this lane's job's running raw CRC
+  uint32_t flags;
+  bool live, active, done;
+  uint32_t pre[16];  // the next super-step's block, in flight
+};
+
+template <int G, int C>
+__device__ __forceinline__ void fed_start(FedLDS<G, C>& L, int c, int lane, FedFeed& F) {
+  FedSlot& P = L.slot[c];
+  F.S = uniform64(P.S);
+  F.flags = uniform32(P.flags);
+  const int m = lane / G, i = lane % G;
+  const DeepMsg& M = L.msg[c][m];
+  F.live = M.live != 0 && M.joint != 0;
+  F.q = M.q + 64 * (M.done + (uint64_t)i);
+  F.crc = M.crc_raw;
+  F.st = 0;
+  F.active = true;
+  fed_load(F.q, F.live, (F.flags & 4u) != 0, F.pre);
+}
+
+// Produce super-step F.st of chain wave c into its (free) slot.
+template <int G, int C>
+__device__ __forceinline__ void fed_produce(FedLDS<G, C>& L, int c, int lane, FedFeed& F) {
+  constexpr int kLG = FedCfg<G, C>::kLG;
+  FedSlot& P = L.slot[c];
+  const bool do_sha = (F.flags & 1u) != 0, do_crc = (F.flags & 2u) != 0, a16 = (F.flags & 4u) != 0;
+  uint32_t cur[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) cur[k] = F.pre[k];
+  if (F.st + 1 < F.S) fed_load(F.q + 64 * G * (F.st + 1), F.live, a16, F.pre);
+  if (do_crc) {
+    uint32_t r = crc_block_pos(L.pos.pos, cur);  // raw CRC of this lane's block (independent lookups)
+#pragma unroll
+    for (int k = 0; k < kLG; ++k) {  // the job's G blocks: crc(A||B) = shift(crc(A), |B|) ^ crc(B)
+      const uint32_t o = __shfl_xor(r, 1 << k);
+      const bool right = (lane >> k) & 1;
+      r = crc_shift(L.tab.shift[k], right ? o : r) ^ (right ? r : o);
+    }
+    F.crc = crc_shift(L.tab.shift[kLG], F.crc) ^ r;  // running CRC advanced over G * 64 bytes
+  }
+  if (do_sha) {
+    uint32_t w[16], x[80];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) w[k] = bswap(cur[k]);
+    expand_wk(w, x);
+#pragma unroll
+    for (int k = 0; k < 20; ++k) P.wk[k][lane] = make_uint4(x[4 * k], x[4 * k + 1], x[4 * k + 2], x[4 * k + 3]);
+    lds_rel32(&P.ready, F.gstep + 1);
+  }
+  ++F.gstep;
+  if (++F.st == F.S) {  // round done: CRCs back to the jobs' messages
+    const int m = lane / G;
+    if (F.live && (lane % G) == 0 && do_crc) L.msg[c][m].crc_raw = F.crc;
+    ++F.round;
+    lds_rel32(&P.crc_done, F.round);
+    F.active = false;
+  }
+}
+
+// Producer p serves chain waves p, p + producers, ... (those of the C that exist: nchains).
+template <int G, int C>
+__device__ void fed_producer(FedLDS<G, C>& L, int lane, int p, uint32_t nchains) {
+  constexpr int kP = FedCfg<G, C>::kProducers;
+  FED_STAT(unsigned long long t_prod = 0, n_prod = 0; const unsigned long long t_begin = __builtin_amdgcn_s_memtime();)
+  FedFeed F[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    F[c].gstep = 0;
+    F[c].round = 0;
+    F[c].active = false;
+    F[c].done = c % kP != p || (uint32_t)c >= nchains;
+  }
+  for (;;) {
+    bool all_done = true, did = false;
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      if (F[c].done) continue;
+      all_done = false;
+      FedSlot& P = L.slot[c];
+      if (!F[c].active) {
+        if (!reached(F[c].round, lds_acq32(&P.req))) {
+          fed_start(L, c, lane, F[c]);
+        } else {
+          if (lds_acq32(&P.fin)) F[c].done = true;
+          continue;
+        }
+      }
+      if ((F[c].flags & 1u) && !reached(lds_acq32(&P.taken), F[c].gstep)) continue;  // slot still in use
+      FED_STAT(const unsigned long long t0 = __builtin_amdgcn_s_memtime();)
+      fed_produce(L, c, lane, F[c]);
+      FED_STAT(t_prod += __builtin_amdgcn_s_memtime() - t0; ++n_prod;)
+      did = true;
+    }
+    if (all_done) break;
+    if (!did) __builtin_amdgcn_s_sleep(1);
+  }
+#ifdef EFES_FED_STATS
+  if (blockIdx.x == 0 && lane == 0 && p == 0) {
+    unsigned hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    g_fed_stats[12] = t_prod;
+    g_fed_stats[13] = n_prod;
+    g_fed_stats[14] = __builtin_amdgcn_s_memtime() - t_begin;
+    g_fed_stats[15] = hw;
+  }
+#endif
+}
+
+// Chain side of one round: S super-steps of G blocks for every joint job of the wave.
+template <int G>
+__device__ void fed_consume(FedSlot& P, int lane, const DeepMsg* msgs, uint64_t S, uint32_t& gstep, uint32_t (&hv)[5],
+                            unsigned long long* stats) {
+  (void)stats;
+  const DeepMsg& M = msgs[lane / G];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) hv[k] = M.h[k];
+  uint32_t hs[5] = {0, 0, 0, 0, 0};
+  FED_STAT(const unsigned long long t_begin = __builtin_amdgcn_s_memtime();)
+  for (uint64_t st = 0; st < S; ++st) {
+    FED_STAT(const unsigned long long t0 = __builtin_amdgcn_s_memtime();)
+    while (!reached(lds_acq32(&P.ready), gstep + 1)) __builtin_amdgcn_s_sleep(1);
+    FED_STAT(stats[0] += __builtin_amdgcn_s_memtime() - t0;)
+    uint32_t x[80];
+#pragma unroll
+    for (int k = 0; k < 20; ++k) {
+      const uint4 v = P.wk[k][lane];
+      x[4 * k] = v.x; x[4 * k + 1] = v.y; x[4 * k + 2] = v.z; x[4 * k + 3] = v.w;
+    }
+    lds_rel32(&P.taken, gstep + 1);  // the producer may overwrite the slot now
+    ++gstep;
+    auto block = [&]() {
+      uint32_t s[5] = {hv[0], hv[1], hv[2], hv[3], hv[4]};
+      ChainRegs<0>::run(s, x);  // real in lane m*G+j of every job m at iteration j
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {
+        hs[k] = hv[k] + s[k];
+        hv[k] = (uint32_t)__builtin_amdgcn_mov_dpp((int)hs[k], 0x138, 0xf, 0xf, true);  // wave_shr:1
+      }
+    };
+#pragma unroll
+    for (int j = 0; j < G; ++j) block();
+#pragma unroll
+    for (int k = 0; k < 5; ++k) hv[k] = (uint32_t)__shfl((int)hs[k], lane | (G - 1));
+  }
+  FED_STAT(stats[1] += __builtin_amdgcn_s_memtime() - t_begin; stats[2] += S;)
+}
+
+template <int G, int C>
+__global__ __launch_bounds__(256, 1) void fed_kernel(const efes_job* __restrict__ jobs, uint32_t njobs,
+                                                     const Tables* __restrict__ tabs) {
+  constexpr int kJobs = FedCfg<G, C>::kJobs;
+  __shared__ __attribute__((aligned(16))) FedLDS<G, C> L;
+  static_assert(sizeof(FedLDS<G, C>) <= 160 * 1024, "one FED workgroup per CU");
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(tabs);  // Tables, then PosTables (efes_ctx_create)
+    uint4* dst = reinterpret_cast<uint4*>(&L.tab);
+    for (int i = threadIdx.x; i < (int)(sizeof(FedTables) / 16); i += blockDim.x) dst[i] = src[i];
+    const uint4* psrc = reinterpret_cast<const uint4*>(tabs + 1);
+    uint4* pdst = reinterpret_cast<uint4*>(&L.pos);
+    for (int i = threadIdx.x; i < (int)(sizeof(PosTables) / 16); i += blockDim.x) pdst[i] = psrc[i];
+    if (threadIdx.x < C) {
+      FedSlot& P = L.slot[threadIdx.x];
+      P.req = P.fin = P.ready = P.taken = P.crc_done = 0;
+    }
+  }
+  __syncthreads();
+  const int wave = (int)uniform32(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const uint32_t base = blockIdx.x * (uint32_t)(C * kJobs);
+  if (wave >= C) {  // ---- producer (a SIMD of its own)
+    const uint32_t left = njobs - base;  // base < njobs for every launched workgroup
+    fed_producer(L, lane, wave - C, (left + kJobs - 1) / kJobs);
+    return;
+  }
+  // ---- chain wave
+  __builtin_amdgcn_s_setprio(3);
+  const uint32_t j0 = base + (uint32_t)wave * kJobs;
+  if (j0 >= njobs) return;  // no producer waits for this chain wave (nchains above)
+  FedSlot& P = L.slot[wave];
+  DeepMsg* msgs = L.msg[wave];
+  const Tables& T = reinterpret_cast<const Tables&>(L.tab);  // slice8 only (deep_head, deep_rest<false>)
+  for (int m = 0; m < kJobs; ++m) {  // heads (state parked in LDS)
+    const uint32_t j = j0 + (uint32_t)m;
+    DeepMsg M{};
+    if (j < njobs) M = deep_head(T, lane, load_job(jobs, j, lane), L.xs[wave][m]);
+    wave_lds_sync();
+    if (lane == 0) msgs[m] = M;
+  }
+  wave_lds_sync();
+  // Joint rounds as in group_kernel, but down to a single job: a lone job still runs at the fed
+  // chain's latency, and afterwards every job has fewer than G bulk blocks left.
+  uint32_t gstep = 0;
+  unsigned long long stats[3] = {0, 0, 0};
+  for (uint32_t round = 0; round < (uint32_t)kJobs; ++round) {
+    uint64_t S = ~0ull;
+    int joiners = 0;
+    bool any_sha = false, any_crc = false, all16 = true;
+    for (int m = 0; m < kJobs; ++m) {
+      const DeepMsg M = uniform_msg(msgs[m]);
+      const uint64_t left = M.live ? (M.nbulk - M.done) / G : 0;
+      if (left == 0) continue;
+      ++joiners;
+      S = left < S ? left : S;
+      const DeepJob J = load_job(jobs, j0 + (uint32_t)m, lane);
+      any_sha |= J.st != nullptr;
+      any_crc |= J.cs != nullptr;
+      all16 &= (reinterpret_cast<uintptr_t>(M.q + 64 * M.done) & 15) == 0;
+    }
+    if (joiners == 0) break;
+    for (int m = 0; m < kJobs; ++m) {
+      const DeepMsg M = uniform_msg(msgs[m]);
+      if (lane == 0) msgs[m].joint = M.live && (M.nbulk - M.done) / G > 0 ? 1u : 0u;
+    }
+    if (lane == 0) {
+      P.S = S;
+      P.flags = (any_sha ? 1u : 0u) | (any_crc ? 2u : 0u) | (all16 ? 4u : 0u);
+    }
+    lds_rel32(&P.req, round + 1);  // release: the messages and S above are visible first
+    uint32_t hv[5] = {0, 0, 0, 0, 0};
+    if (any_sha) fed_consume<G>(P, lane, msgs, S, gstep, hv, stats);
+    while (!reached(lds_acq32(&P.crc_done), round + 1)) __builtin_amdgcn_s_sleep(1);
+    const int m = lane / G;
+    const bool joint = msgs[m].joint != 0;
+    wave_lds_sync();
+    if (joint && (lane % G) == 0) {
+      DeepMsg& W = msgs[m];
+#pragma unroll
+      for (int k = 0; k < 5; ++k) W.h[k] = any_sha ? hv[k] : W.h[k];
+      W.done += S * G;
+    }
+    wave_lds_sync();
+  }
+  lds_rel32(&P.fin, 1);
+#ifdef EFES_FED_STATS
+  if (blockIdx.x == 0 && lane == 0) {
+    unsigned hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    g_fed_stats[4 * wave + 0] = stats[0];
+    g_fed_stats[4 * wave + 1] = stats[1];
+    g_fed_stats[4 * wave + 2] = stats[2];
+    g_fed_stats[4 * wave + 3] = hw;
+  }
+#endif
+  for (int m = 0; m < kJobs; ++m) {  // per job: the < G left-over blocks, tail, Sum, write-back
+    const uint32_t j = j0 + (uint32_t)m;
+    if (j >= njobs) break;
+    DeepMsg M = uniform_msg(msgs[m]);
+    if (!M.live) continue;
+    const DeepJob J = load_job(jobs, j, lane);
+    for (; M.done < M.nbulk; ++M.done) {  // one block at a time, the same in every lane
+      uint32_t le[16];
+      load_block_le<false>(M.q + 64 * M.done, le);
+      if (J.cs) M.crc_raw = crc_words_raw(T.slice8, M.crc_raw, le);
+      if (J.st) {
+        uint32_t w[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) w[k] = bswap(le[k]);
+        compress_inline(M.h, w);
+      }
+    }
+    deep_rest<false>(T, lane, J, L.xs[wave][m], L.fin[wave], M);
+  }
+}
+
 // ================================================================== WIDE kernel
 // One lane per job.  Per-lane tail buffers live in LDS with a 68-byte stride (17 dwords:
 // lanes touching the same byte index hit different banks).
@@ -1150,11 +1509,35 @@ hipError_t launch_group(const efes_job* jobs, uint32_t njobs, int G, const Table
   }
 }
 
+// FED shape of a mode: lanes per job and chain waves per workgroup.
+constexpr int kFed4G = 4, kFed4C = 2;
+
+template <int G, int C>
+hipError_t launch_fed_shape(const efes_job* jobs, uint32_t njobs, const Tables* tabs, hipStream_t s) {
+  const uint32_t per = C * (64 / G);
+  return launch_reserving(fed_kernel<G, C>, dim3((njobs + per - 1) / per), dim3(256), true, s, jobs, njobs, tabs);
+}
+
+hipError_t launch_fed(const efes_job* jobs, uint32_t njobs, const Tables* tabs, hipStream_t s) {
+  if (njobs == 0) return hipSuccess;
+  if (const char* e = getenv("EFES_FED_SHAPE")) {  // developer override for calibration: "G,C"
+    if (!strcmp(e, "4,3")) return launch_fed_shape<4, 3>(jobs, njobs, tabs, s);
+    if (!strcmp(e, "8,3")) return launch_fed_shape<8, 3>(jobs, njobs, tabs, s);
+  }
+  return launch_fed_shape<kFed4G, kFed4C>(jobs, njobs, tabs, s);
+}
+
 hipError_t launch_wide(const efes_job* jobs, uint32_t njobs, const Tables* tabs, hipStream_t s, bool exclusive) {
   if (njobs == 0) return hipSuccess;
   const uint32_t per = 64 * kWideWaves;
   return launch_reserving(wide_kernel, dim3((njobs + per - 1) / per), dim3(per), exclusive, s, jobs, njobs, tabs);
 }
+
+#ifdef EFES_FED_STATS
+extern "C" int efes_debug_fed_stats(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fed_stats), sizeof(g_fed_stats)) == hipSuccess ? 0 : -3;
+}
+#endif
 
 hipError_t launch_fill(void* dst, size_t bytes, uint64_t seed, hipStream_t s) {
   const uint64_t nwords = bytes / 8;

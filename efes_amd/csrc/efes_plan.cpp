@@ -9,6 +9,9 @@
 //   GROUPn (64/n jobs / wave)  (410 + o_n/n) x 4.1          (410 n + o_n)/64 x 4.1
 //   (o_n = 665: instructions per super-step besides the chain, measured for n = 4..32)
 //   WIDE  (one lane per job)   740 x 5.1                    740/64 x 5.1 (/1.06 once SIMDs hold 2+ waves)
+//   FED4  (32 jobs per CU)     427 x 4.1                    4 SIMDs x 7005 cyc / (32 jobs x 4 blocks)
+//         (grouped G = 4 with loads/CRC/expansion on two producer SIMDs: DEEP's latency, 1/32 CU
+//          per job; measured 7005 cycles per 4-block super-step, 48.5 ms per 4 MiB job)
 // A DEEP/GROUP wave issues at ~4.1 cycles per instruction alone and gains almost nothing from
 // a second wave on its SIMD (1.06x), so where a long job's wave lands matters: the plan can
 // give the longest jobs CUs of their own (exclusive launch) and run the rest on the others.
@@ -36,23 +39,37 @@ namespace {
 
 constexpr double kCpiDeep = 4.1;    // cycles per instruction, DEEP / GROUP wave alone
 constexpr double kCpiWide = 5.1;    // cycles per instruction, WIDE wave alone (dependent CRC LDS lookups)
+// ... and a lone WIDE wave on CUs of its own while the rest of the chip is busy (configs[3] trace:
+// the 32 MiB class as an exclusive WIDE part beside FED4 and shared WIDE parts ended at 1.153 s,
+// 29 MB/s per lane; profiles/r02_mixtrace/)
+constexpr double kCpiWideExclusive = 7.0;
 constexpr double kWideShare = 1.06; // WIDE throughput of a SIMD holding two waves vs one
 constexpr double kClock = 2.36e9;   // Hz (GRBM_GUI_ACTIVE during DEEP), for est_seconds only
 constexpr int kWideLanes = 0;       // "shape" id of WIDE in the search
+constexpr int kFed = 1;             // "shape" id of FED4 (EFES_MODE_FED4)
+constexpr double kFedJobsPerCu = 32.0;
+constexpr double kFedCyclesPerStep = 7005.0;  // one 4-block super-step of a FED4 chain wave
 
 double step_overhead(int) { return 665.0; }
 double latency(int g) {  // cycles per block of one job
   if (g == kWideLanes) return 740.0 * kCpiWide;
-  return (g == 64 ? 422.0 : 410.0 + step_overhead(g) / g) * kCpiDeep;
+  if (g == kFed) return kFedCyclesPerStep / 4.0;
+  return (g == 64 ? 408.0 : 410.0 + step_overhead(g) / g) * kCpiDeep;  // DEEP: 46.4 ms per 4 MiB
 }
 double work(int g, bool crowded) {  // SIMD cycles per block per job
   if (g == kWideLanes) return 740.0 / 64.0 * kCpiWide / (crowded ? kWideShare : 1.0);
+  if (g == kFed) return 4.0 * kFedCyclesPerStep / (kFedJobsPerCu * 4.0);
   return (g == 64 ? 422.0 : (410.0 * g + step_overhead(g)) / 64.0) * kCpiDeep;
 }
-double waves(int g, double jobs) { return std::ceil(jobs / (g == kWideLanes ? 64.0 : 64.0 / g)); }
+// Waves of a deep part (FED4: its chain waves count as half a workgroup's four SIMDs each).
+double waves(int g, double jobs) {
+  if (g == kFed) return 4.0 * std::ceil(jobs / kFedJobsPerCu);
+  return std::ceil(jobs / (g == kWideLanes ? 64.0 : 64.0 / g));
+}
 int mode_of(int g) {
   switch (g) {
     case kWideLanes: return EFES_MODE_WIDE;
+    case kFed: return EFES_MODE_FED4;
     case 4: return EFES_MODE_GROUP4;
     case 8: return EFES_MODE_GROUP8;
     case 16: return EFES_MODE_GROUP16;
@@ -63,6 +80,7 @@ int mode_of(int g) {
 int lanes_of(int mode) {
   if (mode == EFES_MODE_DEEP) return 64;
   if (mode == EFES_MODE_WIDE) return kWideLanes;
+  if (mode == EFES_MODE_FED4) return kFed;
   return efes::group_of_mode(mode);
 }
 
@@ -110,18 +128,20 @@ int efes_plan_batch(efes_ctx* ctx, const uint64_t* lengths, uint32_t n, uint32_t
 
   // Every DEEP/GROUP part is exclusive (its workgroups own their CUs, so its waves run alone at
   // the lone-wave latency); WIDE runs on the CUs left over and on those the deep parts free.
-  const int shapes[] = {64, 32, 16, 8, 4};
+  // Part 1 may also be WIDE on CUs of its own (one wave per SIMD: its lanes at the lone-wave rate).
+  const int shapes[] = {64, 32, 16, 8, 4, kFed, kWideLanes};
   auto deep_time = [&](int g, uint32_t first, uint32_t jobs, double* cus_out) {
     const double c = std::ceil(waves(g, jobs) / 4.0);
     *cus_out = std::min(c, cus);
-    return blocks(first) * latency(g) * std::ceil(c / cus);  // rounds of workgroups beyond one per CU
+    const double lat = g == kWideLanes ? 740.0 * kCpiWideExclusive : latency(g);
+    return blocks(first) * lat * std::ceil(c / cus);  // rounds of workgroups beyond one per CU
   };
   Cand best;
   double best_work = 0;
   for (size_t a = 0; a < cuts.size(); ++a) {
     const uint32_t d1 = cuts[a];
     for (int g0 : shapes) {
-      if (d1 == 0 && g0 != 64) continue;
+      if (g0 == kWideLanes || (d1 == 0 && g0 != 64)) continue;
       double cus0 = 0;
       const double t0 = d1 ? deep_time(g0, 0, d1, &cus0) : 0.0;
       for (size_t b = a; b < cuts.size(); ++b) {
@@ -176,8 +196,9 @@ int efes_plan_batch(efes_ctx* ctx, const uint64_t* lengths, uint32_t n, uint32_t
 
   // Developer override for calibration runs:
   //   EFES_PLAN_FORCE="<lanes>:<jobs>[x],<lanes>:<jobs>[x],..."  (lanes 64 = DEEP, 0 = WIDE,
-  //   x = exclusive); jobs beyond the listed parts run WIDE (a fourth part is not possible).
-  if (const char* f = getenv("EFES_PLAN_FORCE")) {
+  //   1 = FED4 (always exclusive), x = exclusive); jobs beyond the listed parts run WIDE (a fourth
+  //   part is not possible).
+  if (const char* f = getenv("EFES_PLAN_FORCE"); f && *f) {
     efes_plan_part fp[EFES_PLAN_MAX_PARTS] = {};
     uint32_t fn = 0, used = 0;
     bool ok = true;
@@ -215,7 +236,9 @@ int efes_hash_submit_plan(efes_ctx* ctx, const efes_job* jobs, const efes_plan* 
   uint64_t total = 0;
   for (uint32_t i = 0; i < plan->nparts; ++i) {
     const efes_plan_part& p = plan->part[i];
-    if (p.mode != EFES_MODE_WIDE && p.mode != EFES_MODE_DEEP && !efes::group_of_mode(p.mode)) return EFES_ERR_ARG;
+    if (p.mode != EFES_MODE_WIDE && p.mode != EFES_MODE_DEEP && p.mode != EFES_MODE_FED4 &&
+        !efes::group_of_mode(p.mode))
+      return EFES_ERR_ARG;
     total += p.jobs;
   }
   if (total != plan->njobs) return EFES_ERR_ARG;
@@ -224,6 +247,7 @@ int efes_hash_submit_plan(efes_ctx* ctx, const efes_job* jobs, const efes_plan* 
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
   auto launch = [&](const efes_plan_part& p, const efes_job* first, hipStream_t st) {
     if (p.mode == EFES_MODE_WIDE) return efes::launch_wide(first, p.jobs, ctx->d_tabs, st, p.exclusive != 0);
+    if (p.mode == EFES_MODE_FED4) return efes::launch_fed(first, p.jobs, ctx->d_tabs, st);
     return efes::launch_group(first, p.jobs, lanes_of(p.mode), ctx->d_tabs, st, p.exclusive != 0);
   };
   std::lock_guard<std::mutex> lk(ctx->plan_mu);

@@ -115,6 +115,11 @@ typedef struct efes_job {
 #define EFES_MODE_GROUP8 4
 #define EFES_MODE_GROUP16 5
 #define EFES_MODE_GROUP32 6
+/* FED4: grouped DEEP (16 jobs of 4 lanes per chain wave) whose loads, CRC and schedule
+ * expansion run on a producer wave on another SIMD of the same CU, so a job advances at DEEP's
+ * per-block latency; 48 jobs per workgroup, each workgroup owns its CU.  For the longest jobs of
+ * a mixed batch (efes_plan_batch), more of them than SIMDs. */
+#define EFES_MODE_FED4 7
 
 /* Largest job count of one submit / plan / host batch (larger counts: EFES_ERR_ARG; split the
  * batch).  Keeps every grid size and lane index of the kernels within 32 bits. */
@@ -125,7 +130,8 @@ typedef struct efes_job {
 int efes_hash_submit(efes_ctx* ctx, const efes_job* jobs_device, uint32_t njobs, void* stream);
 int efes_hash_submit_mode(efes_ctx* ctx, const efes_job* jobs_device, uint32_t njobs, void* stream, int mode);
 /* The shape EFES_MODE_AUTO picks for njobs jobs of similar length (ctx may be NULL: one
- * MI355X): DEEP up to one job per SIMD, then GROUP32..GROUP4, WIDE beyond 24 jobs per SIMD. */
+ * MI355X): DEEP up to one job per SIMD, FED4 up to 8 per SIMD (32 per CU), GROUP4 up to 24 per
+ * SIMD, WIDE beyond. */
 int efes_auto_mode(const efes_ctx* ctx, uint32_t njobs);
 /* Mixed-length batches (BASELINE configs[3], concurrent uploads of different sizes): the
  * makespan is set by the longest jobs (a SHA-1 chain per job), so a batch is cut, longest

@@ -170,10 +170,11 @@ int main(void) {
 
 
 def test_auto_mode_by_job_count(efes_lib):
-    """efes_auto_mode (ctx NULL = one MI355X, 1024 SIMDs): DEEP, GROUP32..GROUP4, then WIDE."""
+    """efes_auto_mode (ctx NULL = one MI355X, 1024 SIMDs): DEEP, FED4, GROUP4, then WIDE."""
     L = efes_lib.lib()
     G = efes_lib.MODE_GROUP
-    want = {1: efes_lib.MODE_DEEP, 1024: efes_lib.MODE_DEEP, 1025: G[32], 2048: G[32], 4096: G[16], 8192: G[8],
+    F = efes_lib.MODE_FED4
+    want = {1: efes_lib.MODE_DEEP, 1024: efes_lib.MODE_DEEP, 1025: F, 2048: F, 4096: F, 8192: F,
             8193: G[4], 24576: G[4], 24577: efes_lib.MODE_WIDE, 131072: efes_lib.MODE_WIDE}
     assert {n: L.efes_auto_mode(None, n) for n in want} == want
 

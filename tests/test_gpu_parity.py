@@ -27,13 +27,14 @@ def env():
                 ctx=ctx)
 
 
-MODE_IDS = ["deep", "wide", "group4", "group8", "group16", "group32", "plan"]
+MODE_IDS = ["deep", "wide", "group4", "group8", "group16", "group32", "fed4", "plan"]
 
 
 def _modes(env):
     from efes_amd._lib import MODE_GROUP
     from efes_amd.batch import MODE_PLAN
-    m = {"deep": env["efes"].MODE_DEEP, "wide": env["efes"].MODE_WIDE, "plan": MODE_PLAN}
+    from efes_amd._lib import MODE_FED4
+    m = {"deep": env["efes"].MODE_DEEP, "wide": env["efes"].MODE_WIDE, "plan": MODE_PLAN, "fed4": MODE_FED4}
     m.update({f"group{g}": v for g, v in MODE_GROUP.items()})
     return m
 
@@ -242,7 +243,7 @@ def test_many_small_jobs_auto(env, oracle):
     host = oracle.fill_synthetic(int(lengths.sum()) + 8, 1234)
     buf = device_buffer(env, host)
     b = env["DeviceBatch"](buf.data_ptr(), offsets, lengths, ctx=env["ctx"])
-    b.run()  # AUTO -> GROUP16 at this count (efes_auto_mode)
+    b.run()  # AUTO -> FED4 at this count (efes_auto_mode)
     assert (b.status_host() == 0).all()
     shas, crcs = b.sha1_hex(), b.crc_sum()
     for i in range(0, n, 7):
@@ -807,15 +808,17 @@ def test_host_ingest_zero_copy(env, oracle):
     assert e.value.code == env["efes"].EFES_ERR_ARG
 
 
-@pytest.mark.parametrize("lanes", [4, 8, 16, 32])
+@pytest.mark.parametrize("lanes", [4, 8, 16, 32, "fed4"])
 def test_group_joint_phase_mixed_lengths_and_states(env, oracle, lanes):
     """Grouped DEEP: jobs of one wave with different lengths, offsets and mid-stream states.
 
     Lengths are long enough for the joint phase (S > 0) and leave per-job left-over blocks,
     heads (nx != 0) and tails; some waves mix in short jobs that the cost model keeps out of
     the joint phase.  Wave j holds jobs [j*64/lanes, (j+1)*64/lanes)."""
-    from efes_amd._lib import MODE_GROUP
-    rng = np.random.default_rng(lanes)
+    from efes_amd._lib import MODE_FED4, MODE_GROUP
+    mode = MODE_FED4 if lanes == "fed4" else MODE_GROUP[lanes]
+    lanes = 4 if lanes == "fed4" else lanes  # FED4: the grouped layout of GROUP4, fed from another SIMD
+    rng = np.random.default_rng(lanes + (mode == MODE_FED4))
     n = 3 * (64 // lanes) + 5  # three full waves and a partial one
     lengths = []
     for i in range(n):
@@ -832,9 +835,9 @@ def test_group_joint_phase_mixed_lengths_and_states(env, oracle, lanes):
     buf = device_buffer(env, host)
     states, crcs = midstream_states(oracle, env, n, random.Random(lanes))
     b = env["DeviceBatch"](buf.data_ptr(), offsets, lengths, states=states, crcs=crcs, ctx=env["ctx"])
-    b.run(MODE_GROUP[lanes])
+    b.run(mode)
     datas = [host[o:o + L].tobytes() for o, L in zip(offsets, lengths)]
-    check_batch(b, oracle, datas, states, crcs, what=f"group{lanes}")
+    check_batch(b, oracle, datas, states, crcs, what=f"mode{mode}-lanes{lanes}")
 
 
 @pytest.mark.parametrize("force", ["4:40x", "8:24", "16:10x,4:30", "32:6,8:20", "64:3x", "0:0", "16:1000",

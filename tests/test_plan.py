@@ -5,7 +5,7 @@ The planner orders a batch longest-first and splits it between a DEEP / grouped-
 import numpy as np
 import pytest
 
-from efes_amd._lib import MODE_DEEP, MODE_GROUP, MODE_WIDE
+from efes_amd._lib import MODE_DEEP, MODE_FED4, MODE_GROUP, MODE_WIDE
 from efes_amd.hashing import plan_batch
 
 MiB = 1 << 20
@@ -37,15 +37,15 @@ def test_ingest_config_goes_wide():
 
 
 def test_mixed_config_splits_longest_class_off():
-    """BASELINE configs[3]: ChunkSize 64K..64M -> the longest classes grouped-DEEP on CUs of
+    """BASELINE configs[3]: ChunkSize 64K..64M -> the longest classes in deep shapes on CUs of
     their own, the rest WIDE on the other CUs."""
     sizes = np.asarray([64 << 10 << i for i in range(11)], dtype=np.uint64)
     lengths = sizes[np.random.default_rng(7).integers(0, 11, 65536)]
     order, plan = plan_batch(lengths)
     parts = plan.parts()
     assert len(parts) in (2, 3) and sum(p[0] for p in parts) == 65536
-    for jobs, mode, exclusive in parts[:-1]:  # grouped DEEP on CUs of their own
-        assert mode in MODE_GROUP.values() and exclusive
+    for jobs, mode, exclusive in parts[:-1]:  # deep shapes (or lone-wave WIDE) on CUs of their own
+        assert mode in (MODE_FED4, MODE_WIDE, *MODE_GROUP.values()) and exclusive
     assert parts[-1][1] == MODE_WIDE and not parts[-1][2]
     # cuts fall between lengths: every job of a part is at least as long as every later one
     cut = 0
@@ -56,8 +56,11 @@ def test_mixed_config_splits_longest_class_off():
     assert 0.5 < plan.est_seconds < 2.0
 
 
-def test_more_long_jobs_than_simds_use_groups():
+def test_more_long_jobs_than_simds_use_fed_then_groups():
+    """Up to 32 long jobs per CU: FED4 (DEEP's latency); beyond that grouped DEEP."""
     _, plan = plan_batch([4 * MiB] * 4096)
+    assert len(plan.parts()) == 1 and plan.parts()[0][1] == MODE_FED4
+    _, plan = plan_batch([4 * MiB] * 16384)
     assert len(plan.parts()) == 1 and plan.parts()[0][1] in MODE_GROUP.values()
 
 

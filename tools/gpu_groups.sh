@@ -1,5 +1,5 @@
 # Grouped-DEEP calibration: one wave per SIMD for each lanes-per-job (n jobs x 4 MiB, 64/n jobs per wave).
-cd "$GRAFT_REPO_ROOT" || exit 1
+cd "${GRAFT_REPO_ROOT:?}" || exit 1
 mkdir -p gpurun_out/groups
 one() {  # tag chunks mode
   timeout -k 10 300 python bench.py --chunks $2 --mode $3 --steps 3 --warmup 1 --no-cpu-baseline --host-inclusive off \

@@ -1,6 +1,6 @@
 # BASELINE configs[3] (mixed ChunkSize 64K..64M x 65536) under several placements, one device:
 #   bash tools/gpu_mixed.sh [force ...]    force = "<lanes per job>:<deep jobs>" (EFES_PLAN_FORCE)
-cd "$GRAFT_REPO_ROOT" || exit 1
+cd "${GRAFT_REPO_ROOT:?}" || exit 1
 mkdir -p gpurun_out/mixed
 run() {  # tag, extra env/args
   local tag=$1; shift

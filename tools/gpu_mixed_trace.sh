@@ -1,6 +1,6 @@
 # Kernel trace of planned mixed (configs[3]) runs: per-part kernel start/end and LDS per workgroup.
 #   bash tools/gpu_mixed_trace.sh <force> ...
-cd "$GRAFT_REPO_ROOT" || exit 1
+cd "${GRAFT_REPO_ROOT:?}" || exit 1
 export TMPDIR=/tmp
 mkdir -p gpurun_out/mixtrace
 for f in "$@"; do

@@ -2,7 +2,7 @@
 # One GPU session: smoke -> GPU parity tests -> bench -> rocprofv3 kernel trace -> PMC FETCH_SIZE pass.
 # Stops at the first step that faults, aborts or times out (never retries a GPU step).
 # Usage (from the repo root on the GPU box): bash tools/gpu_round.sh <tag> [steps...]
-cd "$GRAFT_REPO_ROOT" || exit 1
+cd "${GRAFT_REPO_ROOT:?}" || exit 1
 TAG=${1:-r01}; shift
 STEPS=${*:-"smoke tests bench prof pmc"}
 OUT=gpurun_out; mkdir -p $OUT

@@ -168,9 +168,7 @@ void efes_queue::run() {
     // the chain).  Measured 2.5x the rate of staging copies.
     hipError_t e = hipSuccess;
     if (e == hipSuccess) e = hipMemcpyAsync(dj, hj, sizeof(efes_job) * b.items.size(), hipMemcpyHostToDevice, stream);
-    // DEEP (or grouped DEEP beyond one chunk per SIMD): coalesced reads of 4 KiB per wave (G*64 B
-    // per chunk for GROUPn); WIDE's scattered 64-B lane reads are slow over PCIe.
-    // (Measured with 2048 uploads in flight: 35.3-36.5 GiB/s vs 32.0-34.8 for DEEP only.)
+    // DEEP (or grouped DEEP beyond one chunk per SIMD): efes::pcie_mode.
     const uint32_t nb = (uint32_t)b.items.size();
     int rc = e == hipSuccess ? efes_hash_submit_mode(ctx, dj, nb, stream, efes::pcie_mode(ctx, nb)) : EFES_ERR_HIP;
     if (rc == EFES_OK && hipEventCreateWithFlags(&b.ev, hipEventDisableTiming) != hipSuccess) rc = EFES_ERR_HIP;

@@ -58,20 +58,6 @@ hipError_t launch_group(const efes_job* jobs, uint32_t njobs, int G, const Table
 hipError_t launch_fed(const efes_job* jobs, uint32_t njobs, const Tables* tabs, hipStream_t s);
 hipError_t launch_fill(void* dst, size_t bytes, uint64_t seed, hipStream_t s);
 
-// Kernel shape for jobs whose bytes are read over PCIe in place (pinned, device-mapped host
-// memory): the lowest-latency shape that keeps each job's reads long -- DEEP (4 KiB per job per
-// super-step), then grouped DEEP with as many lanes per job as fit (G*64 contiguous bytes);
-// never WIDE (scattered 64-B lane reads) nor FED4 (256 B per job, like GROUP4, at 32 jobs per CU).
-// (Measured with 2048 uploads in flight: grouped 35.3-36.5 GiB/s vs 32.0-34.8 for DEEP only.)
-inline int pcie_mode(const efes_ctx* ctx, uint32_t njobs) {
-  const uint64_t simds = 4ull * (ctx ? (uint64_t)ctx->cus : 256ull), n = njobs;
-  if (n <= simds) return EFES_MODE_DEEP;
-  if (n <= 2 * simds) return EFES_MODE_GROUP32;
-  if (n <= 4 * simds) return EFES_MODE_GROUP16;
-  if (n <= 8 * simds) return EFES_MODE_GROUP8;
-  return EFES_MODE_GROUP4;
-}
-
 // Lanes per job of a grouped-DEEP mode (EFES_MODE_GROUPn -> n), 0 for other modes.
 inline int group_of_mode(int mode) {
   switch (mode) {
@@ -114,3 +100,21 @@ struct efes_ctx {
   std::mutex mu;                  // guards the lazy creation of `digests`
   efes_queue* digests = nullptr;  // shared queue of the streaming digests (efes_stream.cpp)
 };
+
+namespace efes {
+
+// Kernel shape for jobs whose bytes are read over PCIe in place (pinned, device-mapped host
+// memory): the lowest-latency shape that keeps each job's reads long -- DEEP (4 KiB per job per
+// super-step), then grouped DEEP with as many lanes per job as fit (G*64 contiguous bytes);
+// never WIDE (scattered 64-B lane reads) nor FED4 (256 B per job, like GROUP4, at 32 jobs per CU).
+// (Measured with 2048 uploads in flight: grouped 35.3-36.5 GiB/s vs 32.0-34.8 for DEEP only.)
+inline int pcie_mode(const efes_ctx* ctx, uint32_t njobs) {
+  const uint64_t simds = 4ull * (ctx ? (uint64_t)ctx->cus : 256ull), n = njobs;
+  if (n <= simds) return EFES_MODE_DEEP;
+  if (n <= 2 * simds) return EFES_MODE_GROUP32;
+  if (n <= 4 * simds) return EFES_MODE_GROUP16;
+  if (n <= 8 * simds) return EFES_MODE_GROUP8;
+  return EFES_MODE_GROUP4;
+}
+
+}  // namespace efes

@@ -71,6 +71,8 @@ def parse_args(argv=None):
     p.add_argument("--segment-bytes", type=int, default=256 << 10, help="host-inclusive pipeline segment")
     p.add_argument("--ingest-leg", choices=["auto", "on", "off"], default="auto",
                    help="also report BASELINE configs[4] per-GPU (auto = N=1 only)")
+    p.add_argument("--concurrency-leg", choices=["auto", "on", "off"], default="auto",
+                   help="also report 4 MiB chunks at 1K..192K in flight, one AUTO launch each (auto = N=1 only)")
     p.add_argument("--mixed-leg", choices=["auto", "on", "off"], default="auto",
                    help="also report BASELINE configs[3] (planned mixed-size batch); auto = N=1 only")
     p.add_argument("--dist-backend", default="nccl", help="N>1 timing barrier/max only (no data-path collective)")
@@ -364,6 +366,38 @@ def ingest_leg(args, rank: int, world: int, ctx, device: str, stream, mode: int)
             "note": "many concurrent chunks per GPU (configs[4] per-GPU queue); not `value`"}
 
 
+def concurrency_leg(args, ctx, device: str, stream):
+    """How the rate of 4 MiB chunks depends on how many are in flight: one AUTO
+    launch per count (DEEP up to one chunk per SIMD, FED4 up to 32 per CU, GROUP4, then WIDE),
+    chunks aliasing a 64 GiB device pool; one warm-up and two timed launches per point."""
+    import numpy as np
+    import torch
+
+    from efes_amd._lib import MODE_AUTO, MODE_FED4, MODE_GROUP, lib
+    from efes_amd.batch import DeviceBatch
+    from efes_amd import MODE_DEEP, MODE_WIDE
+
+    names = {MODE_DEEP: "deep_kernel", MODE_WIDE: "wide_kernel", MODE_FED4: "fed_kernel"}
+    names.update({v: f"group_kernel<{g}>" for g, v in MODE_GROUP.items()})
+    chunk, pool = 4 << 20, 64 << 30
+    points = []
+    with torch.cuda.stream(stream):
+        data = torch.empty(pool, dtype=torch.uint8, device=device)
+        ctx.fill_synthetic(data.data_ptr(), pool, 0xC0C0, stream.cuda_stream)
+        slots = pool // chunk
+        for n in (1024, 2048, 4096, 8192, 16384, 65536, 196608):
+            b = DeviceBatch(data.data_ptr(), (np.arange(n, dtype=np.uint64) % np.uint64(slots)) * np.uint64(chunk),
+                            np.full(n, chunk), fresh=True, ctx=ctx, device=device)
+            wall, kernel_ms = run_timed([b], 2, 1, MODE_AUTO, device, stream, None)
+            points.append({"chunks": n, "kernel": names[lib().efes_auto_mode(ctx.handle, n)],
+                           "GiB/s": round(2 * n * chunk / wall / GiB, 1), "ms_per_launch": round(kernel_ms, 2)})
+            del b
+        del data
+        torch.cuda.empty_cache()
+    return {"unit": "GiB/s", "chunk_bytes": chunk, "points": points,
+            "note": "one launch of n fresh 4 MiB chunks (fused SHA-1+CRC32), AUTO shape; not `value`"}
+
+
 def mixed_leg(args, rank: int, world: int, ctx, device: str, stream):
     """BASELINE configs[3] beside the metric: 65 536 chunks of the eleven ChunkSize values
     64K..64M (752 GiB, aliasing a 64 GiB pool), placed by efes_plan_batch (grouped-DEEP parts
@@ -504,6 +538,8 @@ def main(argv=None):
                                                    batches[0])
         if args.ingest_leg == "on" or (args.ingest_leg == "auto" and world == 1):
             out["ingest_config"] = ingest_leg(args, rank, world, ctx, device, stream, MODE_AUTO)
+        if args.concurrency_leg == "on" or (args.concurrency_leg == "auto" and world == 1):
+            out["concurrency"] = concurrency_leg(args, ctx, device, stream)
         if args.mixed_leg == "on" or (args.mixed_leg == "auto" and world == 1):
             out["mixed_config"] = mixed_leg(args, rank, world, ctx, device, stream)
         if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -648,6 +648,8 @@ def test_bench_emits_driver_json(env):
     assert d["steps"] == 2 and d["n_gpus"] == 1 and d["value"] > 0
     assert d["roofline"]["bound"] == "hbm" and 0 < d["roofline"]["frac"] < 1
     assert d["cpu_baseline"]["digests_match_gpu"] and d["host_inclusive"]["digests_match_device_path"]
+    kernels = [p["kernel"] for p in d["concurrency"]["points"]]
+    assert kernels[:2] == ["deep_kernel", "fed_kernel"] and kernels[-1] == "wide_kernel"
 
 
 def test_streaming_digests_batch_across_threads(env, oracle):

@@ -36,6 +36,17 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-leve
 GiB = 1 << 30
 
 
+def kernel_names() -> dict:
+    """Kernel (rocprof name) of each EFES_MODE_* shape."""
+    from efes_amd import MODE_DEEP, MODE_WIDE
+    from efes_amd._lib import MODE_FED4, MODE_FED4E, MODE_GROUP
+
+    names = {MODE_DEEP: "deep_kernel", MODE_WIDE: "wide_kernel", MODE_FED4: "fed_kernel<4, 2>",
+             MODE_FED4E: "fed_kernel<4, 3>"}
+    names.update({v: f"group_kernel<{g}>" for g, v in MODE_GROUP.items()})
+    return names
+
+
 def parse_args(argv=None):
     p = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     p.add_argument("--gpus", type=int, default=1)
@@ -43,7 +54,8 @@ def parse_args(argv=None):
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--chunks", type=int, default=1024, help="chunks per GPU")
     p.add_argument("--chunk-bytes", type=int, default=4 << 20)
-    p.add_argument("--mode", choices=["auto", "deep", "wide", "plan", "group4", "group8", "group16", "group32", "fed4"],
+    p.add_argument("--mode", choices=["auto", "deep", "wide", "plan", "group4", "group8", "group16", "group32", "fed4",
+                                       "fed4e"],
                    default="auto", help="auto: AUTO for chunks4m/ingest, plan (efes_plan_batch) for mixed")
     p.add_argument("--workload", choices=["chunks4m", "mixed", "ingest", "uploads"], default="chunks4m",
                    help="chunks4m = BASELINE configs[1]/[2] (the metric); mixed = configs[3]; ingest = configs[4]")
@@ -368,17 +380,16 @@ def ingest_leg(args, rank: int, world: int, ctx, device: str, stream, mode: int)
 
 def concurrency_leg(args, ctx, device: str, stream):
     """How the rate of 4 MiB chunks depends on how many are in flight: one AUTO
-    launch per count (DEEP up to one chunk per SIMD, FED4 up to 32 per CU, GROUP4, then WIDE),
+    launch per count (DEEP up to one chunk per SIMD, FED4 / FED4E up to 32 / 48 per CU, GROUP4,
+    then WIDE),
     chunks aliasing a 64 GiB device pool; one warm-up and two timed launches per point."""
     import numpy as np
     import torch
 
-    from efes_amd._lib import MODE_AUTO, MODE_FED4, MODE_GROUP, lib
+    from efes_amd._lib import MODE_AUTO, lib
     from efes_amd.batch import DeviceBatch
-    from efes_amd import MODE_DEEP, MODE_WIDE
 
-    names = {MODE_DEEP: "deep_kernel", MODE_WIDE: "wide_kernel", MODE_FED4: "fed_kernel"}
-    names.update({v: f"group_kernel<{g}>" for g, v in MODE_GROUP.items()})
+    names = kernel_names()
     chunk, pool = 4 << 20, 64 << 30
     points = []
     with torch.cuda.stream(stream):
@@ -406,7 +417,6 @@ def mixed_leg(args, rank: int, world: int, ctx, device: str, stream):
 
     import torch
 
-    from efes_amd._lib import MODE_DEEP, MODE_FED4, MODE_GROUP, MODE_WIDE
     from efes_amd.batch import MODE_PLAN
 
     a = _ap.Namespace(**vars(args))
@@ -417,8 +427,7 @@ def mixed_leg(args, rank: int, world: int, ctx, device: str, stream):
             b.make_plan()
         wall, kernel_ms = run_timed(batches, len(batches), 1, MODE_PLAN, device, stream, None)
     total = sum(step_bytes)
-    names = {MODE_DEEP: "deep_kernel", MODE_WIDE: "wide_kernel", MODE_FED4: "fed_kernel"}
-    names.update({v: f"group_kernel<{g}>" for g, v in MODE_GROUP.items()})
+    names = kernel_names()
     parts = [{"jobs": j, "kernel": names[m], "exclusive_cus": x} for j, m, x in batches[0].plan.parts()]
     achieved = total / len(batches) / (kernel_ms * 1e-3) / 1e9
     del data, batches
@@ -435,7 +444,7 @@ def main(argv=None):
     import torch
 
     from efes_amd import MODE_AUTO, MODE_DEEP, MODE_WIDE
-    from efes_amd._lib import MODE_FED4, MODE_GROUP, lib
+    from efes_amd._lib import MODE_FED4, MODE_FED4E, MODE_GROUP, lib
     from efes_amd.batch import MODE_PLAN
     from efes_amd.hashing import default_context
     from efes_amd.shard import env_rank, max_over_ranks
@@ -459,7 +468,7 @@ def main(argv=None):
     stream = torch.cuda.Stream(device=device)
     modes = {"auto": MODE_AUTO, "deep": MODE_DEEP, "wide": MODE_WIDE, "plan": MODE_PLAN}
     modes.update({f"group{g}": v for g, v in MODE_GROUP.items()})
-    modes["fed4"] = MODE_FED4
+    modes["fed4"], modes["fed4e"] = MODE_FED4, MODE_FED4E
     mode = modes["plan" if args.mode == "auto" and args.workload == "mixed" else args.mode]
 
     if args.workload == "uploads":
@@ -483,15 +492,11 @@ def main(argv=None):
     value = world * bytes_timed / wall / GiB
     njobs = batches[0].n
     launched = lib().efes_auto_mode(ctx.handle, njobs) if mode == MODE_AUTO else mode
-    kernel_name = {MODE_DEEP: "deep_kernel", MODE_WIDE: "wide_kernel", MODE_FED4: "fed_kernel"}.get(launched,
-                                                                                                  "group_kernel")
-    if launched in MODE_GROUP.values():
-        kernel_name = f"group_kernel<{ {v: g for g, v in MODE_GROUP.items()}[launched] }>"
+    kernel_name = kernel_names()[launched]
     plan = None
     if mode == MODE_PLAN:
         p0 = batches[0].plan
-        names = {MODE_DEEP: "deep_kernel", MODE_WIDE: "wide_kernel", MODE_FED4: "fed_kernel"}
-        names.update({v: f"group_kernel<{g}>" for g, v in MODE_GROUP.items()})
+        names = kernel_names()
         plan = {"parts": [{"jobs": j, "kernel": names[m], "exclusive_cus": x} for j, m, x in p0.parts()],
                 "model_seconds": round(p0.est_seconds, 4)}
         kernel_name = " + ".join(p["kernel"] for p in plan["parts"]) + " (concurrent streams)"

@@ -33,7 +33,8 @@ EFES_HASH_SHA1, EFES_HASH_CRC32 = 0x1, 0x2
 EFES_HOST_ZERO_COPY = (1 << 64) - 1
 MODE_AUTO, MODE_DEEP, MODE_WIDE = 0, 1, 2
 MODE_GROUP = {4: 3, 8: 4, 16: 5, 32: 6}  # grouped DEEP: lanes per job -> EFES_MODE_GROUPn
-MODE_FED4 = 7  # grouped DEEP fed by a producer wave on another SIMD (EFES_MODE_FED4)
+MODE_FED4 = 7  # grouped DEEP fed by producer waves on other SIMDs (EFES_MODE_FED4: 2 chains + 2 producers)
+MODE_FED4E = 8  # 3 chain waves (which expand the schedule) + 1 producer per CU (EFES_MODE_FED4E)
 
 
 class HostStats(ctypes.Structure):

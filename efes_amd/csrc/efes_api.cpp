@@ -223,12 +223,13 @@ void* efes_ctx_stream(efes_ctx* ctx) { return ctx ? static_cast<void*>(ctx->stre
 int efes_auto_mode(const efes_ctx* ctx, uint32_t njobs) {
   // The lowest per-job latency that fits in one pass: DEEP up to one job per
   // SIMD (46.5 ms per 4 MiB job); FED4 up to 32 jobs per CU (48.5 ms: DEEP's chain, fed from
-  // two producer SIMDs -- below GROUP32/16/8's 49/52/57 ms at 2/4/8 jobs per SIMD); grouped DEEP
-  // G = 4 (67 ms, 64 jobs per CU) up to 24 jobs per SIMD; WIDE beyond, once its lanes (~40 MB/s
-  // each) outrun GROUP4 (which saturates at one wave per SIMD, ~1 TB/s).
+  // two producer SIMDs -- below GROUP32/16/8's 49/52/57 ms at 2/4/8 jobs per SIMD); FED4E up to
+  // 48 per CU (55.5 ms); grouped DEEP G = 4 (67 ms, 64 jobs per CU) up to 24 jobs per SIMD; WIDE
+  // beyond, once its lanes (~40 MB/s each) outrun GROUP4 (which saturates at one wave per SIMD).
   const uint64_t simds = 4ull * (ctx ? (uint64_t)ctx->cus : 256ull), n = njobs;
   if (n <= simds) return EFES_MODE_DEEP;
   if (n <= 8 * simds) return EFES_MODE_FED4;
+  if (n <= 12 * simds) return EFES_MODE_FED4E;  // 55.5 ms, 48 jobs per CU
   if (n <= 24 * simds) return EFES_MODE_GROUP4;
   return EFES_MODE_WIDE;
 }
@@ -241,7 +242,8 @@ int efes_hash_submit_mode(efes_ctx* ctx, const efes_job* jobs, uint32_t njobs, v
   hipStream_t s = pick(ctx, stream);
   if (mode == EFES_MODE_DEEP) return hip_err(efes::launch_deep(jobs, njobs, ctx->d_tabs, s));
   if (mode == EFES_MODE_WIDE) return hip_err(efes::launch_wide(jobs, njobs, ctx->d_tabs, s));
-  if (mode == EFES_MODE_FED4) return hip_err(efes::launch_fed(jobs, njobs, ctx->d_tabs, s));
+  if (mode == EFES_MODE_FED4 || mode == EFES_MODE_FED4E)
+    return hip_err(efes::launch_fed(jobs, njobs, ctx->d_tabs, s, mode == EFES_MODE_FED4E));
   const int lanes = efes::group_of_mode(mode);
   if (lanes) return hip_err(efes::launch_group(jobs, njobs, lanes, ctx->d_tabs, s));
   return EFES_ERR_ARG;

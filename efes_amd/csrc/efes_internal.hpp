@@ -53,9 +53,10 @@ hipError_t launch_wide(const efes_job* jobs, uint32_t njobs, const Tables* tabs,
 // workgroup reserves all LDS of its CU, so no other workgroup shares the CU's SIMDs.
 hipError_t launch_group(const efes_job* jobs, uint32_t njobs, int G, const Tables* tabs, hipStream_t s,
                         bool exclusive = false);
-// Grouped DEEP fed by a producer wave on another SIMD (EFES_MODE_FED4): 48 jobs per workgroup,
-// which always owns its CU.
-hipError_t launch_fed(const efes_job* jobs, uint32_t njobs, const Tables* tabs, hipStream_t s);
+// Grouped DEEP fed by producer waves on the CU's other SIMDs; each workgroup owns its CU.
+// expand = false: EFES_MODE_FED4 (2 chain waves + 2 producers, 32 jobs per CU); true:
+// EFES_MODE_FED4E (3 chain waves that expand the schedule + 1 producer, 48 jobs per CU).
+hipError_t launch_fed(const efes_job* jobs, uint32_t njobs, const Tables* tabs, hipStream_t s, bool expand);
 hipError_t launch_fill(void* dst, size_t bytes, uint64_t seed, hipStream_t s);
 
 // Lanes per job of a grouped-DEEP mode (EFES_MODE_GROUPn -> n), 0 for other modes.

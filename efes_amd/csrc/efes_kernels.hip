@@ -909,8 +909,9 @@ __device__ __forceinline__ void fed_start(FedLDS<G, C>& L, int c, int lane, FedF
   fed_load(F.q, F.live, (F.flags & 4u) != 0, F.pre);
 }
 
-// Produce super-step F.st of chain wave c into its (free) slot.
-template <int G, int C>
+// Produce super-step F.st of chain wave c into its (free) slot.  X: the chain wave expands the
+// schedule itself, the producer hands over only the 16 message words (big-endian).
+template <int G, int C, bool X>
 __device__ __forceinline__ void fed_produce(FedLDS<G, C>& L, int c, int lane, FedFeed& F) {
   constexpr int kLG = FedCfg<G, C>::kLG;
   FedSlot& P = L.slot[c];
@@ -930,12 +931,18 @@ __device__ __forceinline__ void fed_produce(FedLDS<G, C>& L, int c, int lane, Fe
     F.crc = crc_shift(L.tab.shift[kLG], F.crc) ^ r;  // running CRC advanced over G * 64 bytes
   }
   if (do_sha) {
-    uint32_t w[16], x[80];
+    uint32_t w[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) w[k] = bswap(cur[k]);
-    expand_wk(w, x);
+    if constexpr (X) {
 #pragma unroll
-    for (int k = 0; k < 20; ++k) P.wk[k][lane] = make_uint4(x[4 * k], x[4 * k + 1], x[4 * k + 2], x[4 * k + 3]);
+      for (int k = 0; k < 4; ++k) P.wk[k][lane] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+    } else {
+      uint32_t x[80];
+      expand_wk(w, x);
+#pragma unroll
+      for (int k = 0; k < 20; ++k) P.wk[k][lane] = make_uint4(x[4 * k], x[4 * k + 1], x[4 * k + 2], x[4 * k + 3]);
+    }
     lds_rel32(&P.ready, F.gstep + 1);
   }
   ++F.gstep;
@@ -949,7 +956,7 @@ __device__ __forceinline__ void fed_produce(FedLDS<G, C>& L, int c, int lane, Fe
 }
 
 // Producer p serves chain waves p, p + producers, ... (those of the C that exist: nchains).
-template <int G, int C>
+template <int G, int C, bool X>
 __device__ void fed_producer(FedLDS<G, C>& L, int lane, int p, uint32_t nchains) {
   constexpr int kP = FedCfg<G, C>::kProducers;
   FED_STAT(unsigned long long t_prod = 0, n_prod = 0; const unsigned long long t_begin = __builtin_amdgcn_s_memtime();)
@@ -978,7 +985,7 @@ __device__ void fed_producer(FedLDS<G, C>& L, int lane, int p, uint32_t nchains)
       }
       if ((F[c].flags & 1u) && !reached(lds_acq32(&P.taken), F[c].gstep)) continue;  // slot still in use
       FED_STAT(const unsigned long long t0 = __builtin_amdgcn_s_memtime();)
-      fed_produce(L, c, lane, F[c]);
+      fed_produce<G, C, X>(L, c, lane, F[c]);
       FED_STAT(t_prod += __builtin_amdgcn_s_memtime() - t0; ++n_prod;)
       did = true;
     }
@@ -998,7 +1005,7 @@ __device__ void fed_producer(FedLDS<G, C>& L, int lane, int p, uint32_t nchains)
 }
 
 // Chain side of one round: S super-steps of G blocks for every joint job of the wave.
-template <int G>
+template <int G, bool X>
 __device__ void fed_consume(FedSlot& P, int lane, const DeepMsg* msgs, uint64_t S, uint32_t& gstep, uint32_t (&hv)[5],
                             unsigned long long* stats) {
   (void)stats;
@@ -1012,12 +1019,23 @@ __device__ void fed_consume(FedSlot& P, int lane, const DeepMsg* msgs, uint64_t 
     while (!reached(lds_acq32(&P.ready), gstep + 1)) __builtin_amdgcn_s_sleep(1);
     FED_STAT(stats[0] += __builtin_amdgcn_s_memtime() - t0;)
     uint32_t x[80];
+    if constexpr (X) {
+      uint32_t w[16];
 #pragma unroll
-    for (int k = 0; k < 20; ++k) {
-      const uint4 v = P.wk[k][lane];
-      x[4 * k] = v.x; x[4 * k + 1] = v.y; x[4 * k + 2] = v.z; x[4 * k + 3] = v.w;
+      for (int k = 0; k < 4; ++k) {
+        const uint4 v = P.wk[k][lane];
+        w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
+      }
+      lds_rel32(&P.taken, gstep + 1);  // the producer may overwrite the slot now
+      expand_wk(w, x);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 20; ++k) {
+        const uint4 v = P.wk[k][lane];
+        x[4 * k] = v.x; x[4 * k + 1] = v.y; x[4 * k + 2] = v.z; x[4 * k + 3] = v.w;
+      }
+      lds_rel32(&P.taken, gstep + 1);  // the producer may overwrite the slot now
     }
-    lds_rel32(&P.taken, gstep + 1);  // the producer may overwrite the slot now
     ++gstep;
     auto block = [&]() {
       uint32_t s[5] = {hv[0], hv[1], hv[2], hv[3], hv[4]};
@@ -1036,7 +1054,7 @@ __device__ void fed_consume(FedSlot& P, int lane, const DeepMsg* msgs, uint64_t 
   FED_STAT(stats[1] += __builtin_amdgcn_s_memtime() - t_begin; stats[2] += S;)
 }
 
-template <int G, int C>
+template <int G, int C, bool X>
 __global__ __launch_bounds__(256, 1) void fed_kernel(const efes_job* __restrict__ jobs, uint32_t njobs,
                                                      const Tables* __restrict__ tabs) {
   constexpr int kJobs = FedCfg<G, C>::kJobs;
@@ -1060,7 +1078,7 @@ __global__ __launch_bounds__(256, 1) void fed_kernel(const efes_job* __restrict_
   const uint32_t base = blockIdx.x * (uint32_t)(C * kJobs);
   if (wave >= C) {  // ---- producer (a SIMD of its own)
     const uint32_t left = njobs - base;  // base < njobs for every launched workgroup
-    fed_producer(L, lane, wave - C, (left + kJobs - 1) / kJobs);
+    fed_producer<G, C, X>(L, lane, wave - C, (left + kJobs - 1) / kJobs);
     return;
   }
   // ---- chain wave
@@ -1108,7 +1126,7 @@ __global__ __launch_bounds__(256, 1) void fed_kernel(const efes_job* __restrict_
     }
     lds_rel32(&P.req, round + 1);  // release: the messages and S above are visible first
     uint32_t hv[5] = {0, 0, 0, 0, 0};
-    if (any_sha) fed_consume<G>(P, lane, msgs, S, gstep, hv, stats);
+    if (any_sha) fed_consume<G, X>(P, lane, msgs, S, gstep, hv, stats);
     while (!reached(lds_acq32(&P.crc_done), round + 1)) __builtin_amdgcn_s_sleep(1);
     const int m = lane / G;
     const bool joint = msgs[m].joint != 0;
@@ -1512,19 +1530,20 @@ hipError_t launch_group(const efes_job* jobs, uint32_t njobs, int G, const Table
 // FED shape of a mode: lanes per job and chain waves per workgroup.
 constexpr int kFed4G = 4, kFed4C = 2;
 
-template <int G, int C>
+template <int G, int C, bool X = false>
 hipError_t launch_fed_shape(const efes_job* jobs, uint32_t njobs, const Tables* tabs, hipStream_t s) {
   const uint32_t per = C * (64 / G);
-  return launch_reserving(fed_kernel<G, C>, dim3((njobs + per - 1) / per), dim3(256), true, s, jobs, njobs, tabs);
+  return launch_reserving(fed_kernel<G, C, X>, dim3((njobs + per - 1) / per), dim3(256), true, s, jobs, njobs, tabs);
 }
 
-hipError_t launch_fed(const efes_job* jobs, uint32_t njobs, const Tables* tabs, hipStream_t s) {
+hipError_t launch_fed(const efes_job* jobs, uint32_t njobs, const Tables* tabs, hipStream_t s, bool expand) {
   if (njobs == 0) return hipSuccess;
   if (const char* e = getenv("EFES_FED_SHAPE")) {  // developer override for calibration: "G,C"
     if (!strcmp(e, "4,3")) return launch_fed_shape<4, 3>(jobs, njobs, tabs, s);
     if (!strcmp(e, "8,3")) return launch_fed_shape<8, 3>(jobs, njobs, tabs, s);
   }
-  return launch_fed_shape<kFed4G, kFed4C>(jobs, njobs, tabs, s);
+  if (expand) return launch_fed_shape<4, 3, true>(jobs, njobs, tabs, s);  // FED4E
+  return launch_fed_shape<kFed4G, kFed4C>(jobs, njobs, tabs, s);          // FED4
 }
 
 hipError_t launch_wide(const efes_job* jobs, uint32_t njobs, const Tables* tabs, hipStream_t s, bool exclusive) {

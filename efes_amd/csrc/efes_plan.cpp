@@ -47,29 +47,33 @@ constexpr double kWideShare = 1.06; // WIDE throughput of a SIMD holding two wav
 constexpr double kClock = 2.36e9;   // Hz (GRBM_GUI_ACTIVE during DEEP), for est_seconds only
 constexpr int kWideLanes = 0;       // "shape" id of WIDE in the search
 constexpr int kFed = 1;             // "shape" id of FED4 (EFES_MODE_FED4)
-constexpr double kFedJobsPerCu = 32.0;
-constexpr double kFedCyclesPerStep = 7005.0;  // one 4-block super-step of a FED4 chain wave
+constexpr int kFedE = 2;            // "shape" id of FED4E (EFES_MODE_FED4E)
+// jobs per CU and cycles of one 4-block chain super-step (tools/fed_stats.py, DESIGN.md §4 FED)
+constexpr double fed_jobs_per_cu(int g) { return g == kFed ? 32.0 : 48.0; }
+constexpr double fed_cycles_per_step(int g) { return g == kFed ? 7005.0 : 8219.0; }
+constexpr bool is_fed(int g) { return g == kFed || g == kFedE; }
 
 double step_overhead(int) { return 665.0; }
 double latency(int g) {  // cycles per block of one job
   if (g == kWideLanes) return 740.0 * kCpiWide;
-  if (g == kFed) return kFedCyclesPerStep / 4.0;
+  if (is_fed(g)) return fed_cycles_per_step(g) / 4.0;
   return (g == 64 ? 408.0 : 410.0 + step_overhead(g) / g) * kCpiDeep;  // DEEP: 46.4 ms per 4 MiB
 }
 double work(int g, bool crowded) {  // SIMD cycles per block per job
   if (g == kWideLanes) return 740.0 / 64.0 * kCpiWide / (crowded ? kWideShare : 1.0);
-  if (g == kFed) return 4.0 * kFedCyclesPerStep / (kFedJobsPerCu * 4.0);
+  if (is_fed(g)) return 4.0 * fed_cycles_per_step(g) / (fed_jobs_per_cu(g) * 4.0);
   return (g == 64 ? 422.0 : (410.0 * g + step_overhead(g)) / 64.0) * kCpiDeep;
 }
 // Waves of a deep part (FED4: its chain waves count as half a workgroup's four SIMDs each).
 double waves(int g, double jobs) {
-  if (g == kFed) return 4.0 * std::ceil(jobs / kFedJobsPerCu);
+  if (is_fed(g)) return 4.0 * std::ceil(jobs / fed_jobs_per_cu(g));
   return std::ceil(jobs / (g == kWideLanes ? 64.0 : 64.0 / g));
 }
 int mode_of(int g) {
   switch (g) {
     case kWideLanes: return EFES_MODE_WIDE;
     case kFed: return EFES_MODE_FED4;
+    case kFedE: return EFES_MODE_FED4E;
     case 4: return EFES_MODE_GROUP4;
     case 8: return EFES_MODE_GROUP8;
     case 16: return EFES_MODE_GROUP16;
@@ -81,6 +85,7 @@ int lanes_of(int mode) {
   if (mode == EFES_MODE_DEEP) return 64;
   if (mode == EFES_MODE_WIDE) return kWideLanes;
   if (mode == EFES_MODE_FED4) return kFed;
+  if (mode == EFES_MODE_FED4E) return kFedE;
   return efes::group_of_mode(mode);
 }
 
@@ -129,7 +134,7 @@ int efes_plan_batch(efes_ctx* ctx, const uint64_t* lengths, uint32_t n, uint32_t
   // Every DEEP/GROUP part is exclusive (its workgroups own their CUs, so its waves run alone at
   // the lone-wave latency); WIDE runs on the CUs left over and on those the deep parts free.
   // Part 1 may also be WIDE on CUs of its own (one wave per SIMD: its lanes at the lone-wave rate).
-  const int shapes[] = {64, 32, 16, 8, 4, kFed, kWideLanes};
+  const int shapes[] = {64, 32, 16, 8, 4, kFed, kFedE, kWideLanes};
   auto deep_time = [&](int g, uint32_t first, uint32_t jobs, double* cus_out) {
     const double c = std::ceil(waves(g, jobs) / 4.0);
     *cus_out = std::min(c, cus);
@@ -196,7 +201,7 @@ int efes_plan_batch(efes_ctx* ctx, const uint64_t* lengths, uint32_t n, uint32_t
 
   // Developer override for calibration runs:
   //   EFES_PLAN_FORCE="<lanes>:<jobs>[x],<lanes>:<jobs>[x],..."  (lanes 64 = DEEP, 0 = WIDE,
-  //   1 = FED4 (always exclusive), x = exclusive); jobs beyond the listed parts run WIDE (a fourth
+  //   1 = FED4, 2 = FED4E (both always exclusive), x = exclusive); jobs beyond the listed parts run WIDE (a fourth
   //   part is not possible).
   if (const char* f = getenv("EFES_PLAN_FORCE"); f && *f) {
     efes_plan_part fp[EFES_PLAN_MAX_PARTS] = {};
@@ -237,7 +242,7 @@ int efes_hash_submit_plan(efes_ctx* ctx, const efes_job* jobs, const efes_plan* 
   for (uint32_t i = 0; i < plan->nparts; ++i) {
     const efes_plan_part& p = plan->part[i];
     if (p.mode != EFES_MODE_WIDE && p.mode != EFES_MODE_DEEP && p.mode != EFES_MODE_FED4 &&
-        !efes::group_of_mode(p.mode))
+        p.mode != EFES_MODE_FED4E && !efes::group_of_mode(p.mode))
       return EFES_ERR_ARG;
     total += p.jobs;
   }
@@ -247,7 +252,8 @@ int efes_hash_submit_plan(efes_ctx* ctx, const efes_job* jobs, const efes_plan* 
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
   auto launch = [&](const efes_plan_part& p, const efes_job* first, hipStream_t st) {
     if (p.mode == EFES_MODE_WIDE) return efes::launch_wide(first, p.jobs, ctx->d_tabs, st, p.exclusive != 0);
-    if (p.mode == EFES_MODE_FED4) return efes::launch_fed(first, p.jobs, ctx->d_tabs, st);
+    if (p.mode == EFES_MODE_FED4 || p.mode == EFES_MODE_FED4E)
+      return efes::launch_fed(first, p.jobs, ctx->d_tabs, st, p.mode == EFES_MODE_FED4E);
     return efes::launch_group(first, p.jobs, lanes_of(p.mode), ctx->d_tabs, st, p.exclusive != 0);
   };
   std::lock_guard<std::mutex> lk(ctx->plan_mu);

@@ -120,6 +120,10 @@ typedef struct efes_job {
  * per-block latency; 48 jobs per workgroup, each workgroup owns its CU.  For the longest jobs of
  * a mixed batch (efes_plan_batch), more of them than SIMDs. */
 #define EFES_MODE_FED4 7
+/* FED4E: FED4 with three chain waves and one producer per CU; the chain waves expand the
+ * schedule themselves (the producer loads, CRCs and hands over the 16 message words): 48 jobs per
+ * CU at a per-job latency between FED4's and GROUP4's. */
+#define EFES_MODE_FED4E 8
 
 /* Largest job count of one submit / plan / host batch (larger counts: EFES_ERR_ARG; split the
  * batch).  Keeps every grid size and lane index of the kernels within 32 bits. */
@@ -130,8 +134,8 @@ typedef struct efes_job {
 int efes_hash_submit(efes_ctx* ctx, const efes_job* jobs_device, uint32_t njobs, void* stream);
 int efes_hash_submit_mode(efes_ctx* ctx, const efes_job* jobs_device, uint32_t njobs, void* stream, int mode);
 /* The shape EFES_MODE_AUTO picks for njobs jobs of similar length (ctx may be NULL: one
- * MI355X): DEEP up to one job per SIMD, FED4 up to 8 per SIMD (32 per CU), GROUP4 up to 24 per
- * SIMD, WIDE beyond. */
+ * MI355X): DEEP up to one job per SIMD, FED4 up to 32 per CU, FED4E up to 48 per CU, GROUP4 up to
+ * 24 per SIMD, WIDE beyond. */
 int efes_auto_mode(const efes_ctx* ctx, uint32_t njobs);
 /* Mixed-length batches (BASELINE configs[3], concurrent uploads of different sizes): the
  * makespan is set by the longest jobs (a SHA-1 chain per job), so a batch is cut, longest

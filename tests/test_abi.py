@@ -170,12 +170,12 @@ int main(void) {
 
 
 def test_auto_mode_by_job_count(efes_lib):
-    """efes_auto_mode (ctx NULL = one MI355X, 1024 SIMDs): DEEP, FED4, GROUP4, then WIDE."""
+    """efes_auto_mode (ctx NULL = one MI355X, 1024 SIMDs): DEEP, FED4, FED4E, GROUP4, then WIDE."""
     L = efes_lib.lib()
     G = efes_lib.MODE_GROUP
-    F = efes_lib.MODE_FED4
-    want = {1: efes_lib.MODE_DEEP, 1024: efes_lib.MODE_DEEP, 1025: F, 2048: F, 4096: F, 8192: F,
-            8193: G[4], 24576: G[4], 24577: efes_lib.MODE_WIDE, 131072: efes_lib.MODE_WIDE}
+    F, FE = efes_lib.MODE_FED4, efes_lib.MODE_FED4E
+    want = {1: efes_lib.MODE_DEEP, 1024: efes_lib.MODE_DEEP, 1025: F, 2048: F, 4096: F, 8192: F, 8193: FE,
+            12288: FE, 12289: G[4], 24576: G[4], 24577: efes_lib.MODE_WIDE, 131072: efes_lib.MODE_WIDE}
     assert {n: L.efes_auto_mode(None, n) for n in want} == want
 
 

@@ -17,7 +17,7 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-MODES = ["deep", "wide", "group4", "group8", "group16", "group32", "fed4", "plan"]
+MODES = ["deep", "wide", "group4", "group8", "group16", "group32", "fed4", "fed4e", "plan"]
 EDGE_LENGTHS = [0, 1, 55, 56, 63, 64, 65, 119, 120, 127, 128, 129, 4031, 4095, 4096, 4097, 4159, 8192,
                 16383, 16384, 16385, 65535, 65536, 65537, 262144 + 63]
 
@@ -29,9 +29,10 @@ def env():
         pytest.skip("no GPU")
     import efes_amd
     from efes_amd import hashing
-    from efes_amd._lib import EFES_JOB_FINALIZE, EFES_JOB_INIT, MODE_FED4, MODE_GROUP
+    from efes_amd._lib import EFES_JOB_FINALIZE, EFES_JOB_INIT, MODE_FED4, MODE_FED4E, MODE_GROUP
     from efes_amd.batch import MODE_PLAN, DeviceBatch, fresh_states
-    modes = {"deep": efes_amd.MODE_DEEP, "wide": efes_amd.MODE_WIDE, "plan": MODE_PLAN, "fed4": MODE_FED4}
+    modes = {"deep": efes_amd.MODE_DEEP, "wide": efes_amd.MODE_WIDE, "plan": MODE_PLAN, "fed4": MODE_FED4,
+             "fed4e": MODE_FED4E}
     modes.update({f"group{g}": v for g, v in MODE_GROUP.items()})
     return dict(torch=torch, ctx=hashing.default_context(0), DeviceBatch=DeviceBatch, fresh_states=fresh_states,
                 modes=modes, FIN=EFES_JOB_FINALIZE, INIT=EFES_JOB_INIT)
@@ -141,7 +142,7 @@ def test_random_batches(env, oracle, mode, seed):
     run_case(env, oracle, seed * 7 + MODES.index(mode), mode, 96)
 
 
-@pytest.mark.parametrize("mode", ["deep", "group4", "fed4", "wide"])
+@pytest.mark.parametrize("mode", ["deep", "group4", "fed4", "fed4e", "wide"])
 def test_random_batch_more_jobs_than_simds(env, oracle, mode):
     """1100 random jobs: more than one wave per SIMD for DEEP, several waves per CU for the others."""
     run_case(env, oracle, 4242 + MODES.index(mode), mode, 1100)

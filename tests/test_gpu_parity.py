@@ -27,14 +27,15 @@ def env():
                 ctx=ctx)
 
 
-MODE_IDS = ["deep", "wide", "group4", "group8", "group16", "group32", "fed4", "plan"]
+MODE_IDS = ["deep", "wide", "group4", "group8", "group16", "group32", "fed4", "fed4e", "plan"]
 
 
 def _modes(env):
     from efes_amd._lib import MODE_GROUP
     from efes_amd.batch import MODE_PLAN
-    from efes_amd._lib import MODE_FED4
-    m = {"deep": env["efes"].MODE_DEEP, "wide": env["efes"].MODE_WIDE, "plan": MODE_PLAN, "fed4": MODE_FED4}
+    from efes_amd._lib import MODE_FED4, MODE_FED4E
+    m = {"deep": env["efes"].MODE_DEEP, "wide": env["efes"].MODE_WIDE, "plan": MODE_PLAN, "fed4": MODE_FED4,
+         "fed4e": MODE_FED4E}
     m.update({f"group{g}": v for g, v in MODE_GROUP.items()})
     return m
 
@@ -649,7 +650,7 @@ def test_bench_emits_driver_json(env):
     assert d["roofline"]["bound"] == "hbm" and 0 < d["roofline"]["frac"] < 1
     assert d["cpu_baseline"]["digests_match_gpu"] and d["host_inclusive"]["digests_match_device_path"]
     kernels = [p["kernel"] for p in d["concurrency"]["points"]]
-    assert kernels[:2] == ["deep_kernel", "fed_kernel"] and kernels[-1] == "wide_kernel"
+    assert kernels[:2] == ["deep_kernel", "fed_kernel<4, 2>"] and kernels[-1] == "wide_kernel"
 
 
 def test_streaming_digests_batch_across_threads(env, oracle):
@@ -810,17 +811,18 @@ def test_host_ingest_zero_copy(env, oracle):
     assert e.value.code == env["efes"].EFES_ERR_ARG
 
 
-@pytest.mark.parametrize("lanes", [4, 8, 16, 32, "fed4"])
+@pytest.mark.parametrize("lanes", [4, 8, 16, 32, "fed4", "fed4e"])
 def test_group_joint_phase_mixed_lengths_and_states(env, oracle, lanes):
     """Grouped DEEP: jobs of one wave with different lengths, offsets and mid-stream states.
 
     Lengths are long enough for the joint phase (S > 0) and leave per-job left-over blocks,
     heads (nx != 0) and tails; some waves mix in short jobs that the cost model keeps out of
     the joint phase.  Wave j holds jobs [j*64/lanes, (j+1)*64/lanes)."""
-    from efes_amd._lib import MODE_FED4, MODE_GROUP
-    mode = MODE_FED4 if lanes == "fed4" else MODE_GROUP[lanes]
-    lanes = 4 if lanes == "fed4" else lanes  # FED4: the grouped layout of GROUP4, fed from another SIMD
-    rng = np.random.default_rng(lanes + (mode == MODE_FED4))
+    from efes_amd._lib import MODE_FED4, MODE_FED4E, MODE_GROUP
+    fed = {"fed4": MODE_FED4, "fed4e": MODE_FED4E}
+    mode = fed.get(lanes) or MODE_GROUP[lanes]
+    lanes = 4 if lanes in fed else lanes  # FED4/FED4E: the grouped layout of GROUP4, fed from other SIMDs
+    rng = np.random.default_rng(lanes + (mode in fed.values()) + (mode == MODE_FED4E))
     n = 3 * (64 // lanes) + 5  # three full waves and a partial one
     lengths = []
     for i in range(n):

@@ -5,7 +5,7 @@ The planner orders a batch longest-first and splits it between a DEEP / grouped-
 import numpy as np
 import pytest
 
-from efes_amd._lib import MODE_DEEP, MODE_FED4, MODE_GROUP, MODE_WIDE
+from efes_amd._lib import MODE_DEEP, MODE_FED4, MODE_FED4E, MODE_GROUP, MODE_WIDE
 from efes_amd.hashing import plan_batch
 
 MiB = 1 << 20
@@ -45,7 +45,7 @@ def test_mixed_config_splits_longest_class_off():
     parts = plan.parts()
     assert len(parts) in (2, 3) and sum(p[0] for p in parts) == 65536
     for jobs, mode, exclusive in parts[:-1]:  # deep shapes (or lone-wave WIDE) on CUs of their own
-        assert mode in (MODE_FED4, MODE_WIDE, *MODE_GROUP.values()) and exclusive
+        assert mode in (MODE_FED4, MODE_FED4E, MODE_WIDE, *MODE_GROUP.values()) and exclusive
     assert parts[-1][1] == MODE_WIDE and not parts[-1][2]
     # cuts fall between lengths: every job of a part is at least as long as every later one
     cut = 0

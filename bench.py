@@ -492,7 +492,7 @@ def main(argv=None):
     value = world * bytes_timed / wall / GiB
     njobs = batches[0].n
     launched = lib().efes_auto_mode(ctx.handle, njobs) if mode == MODE_AUTO else mode
-    kernel_name = kernel_names()[launched]
+    kernel_name = kernel_names().get(launched, "planned parts")  # MODE_PLAN: named from the plan below
     plan = None
     if mode == MODE_PLAN:
         p0 = batches[0].plan

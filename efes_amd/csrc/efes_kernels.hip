@@ -886,7 +886,7 @@ __device__ __forceinline__ void fed_load(const uint8_t* src, bool live, bool a16
 struct FedFeed {
   const uint8_t* q;  // this lane's job: first byte of the round (M.q + 64 * (M.done + i))
   uint64_t S, st;    // super-steps of the round, produced so far
-  uint32_t gstep;    // super-steps produced for this chain wave, all rounds
+  uint32_t gstep;    // W+K super-steps handed to this chain wave, all rounds
   uint32_t round;    // rounds served
   uint32_t crc;      // this lane's job's running raw CRC
   uint32_t flags;
@@ -944,8 +944,8 @@ __device__ __forceinline__ void fed_produce(FedLDS<G, C>& L, int c, int lane, Fe
       for (int k = 0; k < 20; ++k) P.wk[k][lane] = make_uint4(x[4 * k], x[4 * k + 1], x[4 * k + 2], x[4 * k + 3]);
     }
     lds_rel32(&P.ready, F.gstep + 1);
+    ++F.gstep;  // counts handed-over super-steps only, as the chain's copy-outs do
   }
-  ++F.gstep;
   if (++F.st == F.S) {  // round done: CRCs back to the jobs' messages
     const int m = lane / G;
     if (F.live && (lane % G) == 0 && do_crc) L.msg[c][m].crc_raw = F.crc;

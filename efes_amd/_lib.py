@@ -47,7 +47,7 @@ class PlanPart(ctypes.Structure):
                 ("_reserved", ctypes.c_uint32)]
 
 
-PLAN_MAX_PARTS = 3
+PLAN_MAX_PARTS = 4
 
 
 class Plan(ctypes.Structure):

@@ -183,10 +183,10 @@ int efes_ctx_create(int device, efes_ctx** out) {
   ctx->cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
   hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming);
-  for (int i = 0; i < EFES_PLAN_MAX_PARTS - 1 && e == hipSuccess; ++i) {
+  for (int i = 0; i < EFES_PLAN_MAX_PARTS - 1 && e == hipSuccess; ++i)
     e = hipStreamCreateWithFlags(&ctx->side[i], hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_join[i], hipEventDisableTiming);
-  }
+  for (int i = 0; i < EFES_PLAN_MAX_PARTS && e == hipSuccess; ++i)
+    e = hipEventCreateWithFlags(&ctx->ev_join[i], hipEventDisableTiming);
   if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&ctx->d_tabs), tab_bytes);
   if (e == hipSuccess) e = hipMemcpy(ctx->d_tabs, host, tab_bytes, hipMemcpyHostToDevice);
   free(host);

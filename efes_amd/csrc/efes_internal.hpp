@@ -93,9 +93,10 @@ struct efes_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   int cus = 256;                  // compute units (efes_plan_batch's capacity)
-  // side streams of a planned batch (efes_hash_submit_plan): one per part but the last
+  // streams of a planned batch's parts (efes_hash_submit_plan): side[0..2], then `stream`
   hipStream_t side[EFES_PLAN_MAX_PARTS - 1] = {};
-  hipEvent_t ev_fork = nullptr, ev_join[EFES_PLAN_MAX_PARTS - 1] = {};
+  hipEvent_t ev_fork = nullptr, ev_join[EFES_PLAN_MAX_PARTS] = {};
+  hipStream_t part_stream(uint32_t i) const { return i < EFES_PLAN_MAX_PARTS - 1 ? side[i] : stream; }
   std::mutex plan_mu;             // one planned submit at a time uses the side streams/events
   efes::Tables* d_tabs = nullptr;
   std::mutex mu;                  // guards the lazy creation of `digests`

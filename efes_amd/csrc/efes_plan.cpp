@@ -18,9 +18,11 @@
 //
 // Search: longest-first order; cuts d1 <= d2 at length boundaries; part 0 = jobs [0, d1) in
 // shape g0 and part 1 = [d1, d2) in shape g1, each on CUs of its own (exclusive: its waves run
-// alone, at the lone-wave latency); part 2 = [d2, n) WIDE on the CUs left over, joined by the
-// deep parts' CUs as those finish.  Makespan = max(deep latencies, WIDE drain time, longest
-// WIDE job's latency); within 2 % the plan with less total issue work wins.  Measured on the
+// alone, at the lone-wave latency); the rest [d2, n) WIDE on the CUs left over, joined by the
+// exclusive parts' CUs as those finish.  The best such plan may then take a third exclusive part
+// [d2, d3) (e.g. the 16 MiB class of configs[3] as WIDE with one wave per SIMD, whose lanes
+// otherwise share SIMDs and set the tail).  Makespan = max(exclusive latencies, WIDE drain time,
+// longest WIDE job's latency); within 2 % the plan with less total issue work wins.  Measured on the
 // mixed config (configs[3]): WIDE waves sharing SIMDs with deep waves lose to them (older
 // waves issue first), which is why the deep parts get CUs of their own.
 #include <hip/hip_runtime.h>
@@ -31,6 +33,7 @@
 #include <algorithm>
 #include <cmath>
 #include <numeric>
+#include <utility>
 #include <vector>
 
 #include "efes_internal.hpp"
@@ -43,6 +46,10 @@ constexpr double kCpiWide = 5.1;    // cycles per instruction, WIDE wave alone (
 // the 32 MiB class as an exclusive WIDE part beside FED4 and shared WIDE parts ended at 1.153 s,
 // 29 MB/s per lane; profiles/r02_mixtrace/)
 constexpr double kCpiWideExclusive = 7.0;
+// ... and the longest lane of the shared WIDE part on the busy chip, before the x2/1.06 stretch
+// of sharing its SIMD (configs[3] trace: the 16 MiB class of the shared part ended at 0.976 s;
+// profiles/r02_mixtrace/2_6019x-4_6027x.csv)
+constexpr double kCpiWideBusy = 6.0;
 constexpr double kWideShare = 1.06; // WIDE throughput of a SIMD holding two waves vs one
 constexpr double kClock = 2.36e9;   // Hz (GRBM_GUI_ACTIVE during DEEP), for est_seconds only
 constexpr int kWideLanes = 0;       // "shape" id of WIDE in the search
@@ -89,11 +96,6 @@ int lanes_of(int mode) {
   return efes::group_of_mode(mode);
 }
 
-struct Cand {
-  double t = -1;
-  uint32_t d1 = 0, d2 = 0;
-  int g0 = 64, g1 = 64;
-};
 
 }  // namespace
 
@@ -141,68 +143,100 @@ int efes_plan_batch(efes_ctx* ctx, const uint64_t* lengths, uint32_t n, uint32_t
     const double lat = g == kWideLanes ? 740.0 * kCpiWideExclusive : latency(g);
     return blocks(first) * lat * std::ceil(c / cus);  // rounds of workgroups beyond one per CU
   };
-  Cand best;
-  double best_work = 0;
-  for (size_t a = 0; a < cuts.size(); ++a) {
-    const uint32_t d1 = cuts[a];
+  // Makespan of a candidate: exclusive parts ps[0..k) (jobs [previous end, end) in shape g, on
+  // CUs of their own) concurrent with a WIDE part for the remaining jobs, which drains through
+  // the CUs left over and is joined by each exclusive part's CUs as that part ends.
+  struct Part {
+    uint32_t end;
+    int g;
+  };
+  auto evaluate = [&](const Part* ps, int k, double* work_out) -> double {
+    double t = 0, wk = 0, used = 0;
+    std::pair<double, double> fin[EFES_PLAN_MAX_PARTS];  // (end time, CUs) of each exclusive part
+    int nf = 0;
+    uint32_t start = 0;
+    for (int i = 0; i < k; ++i) {
+      if (ps[i].end <= start) continue;
+      double c = 0;
+      const double ti = deep_time(ps[i].g, start, ps[i].end - start, &c);
+      t = std::max(t, ti);
+      wk += (pre[ps[i].end] - pre[start]) * work(ps[i].g, false);
+      used += c;
+      fin[nf++] = {ti, c};
+      start = ps[i].end;
+    }
+    *work_out = wk;
+    if (used > cus || (start < n && used >= cus)) return -1;  // does not fit
+    if (start < n) {
+      const double free0 = 4.0 * (cus - used);
+      const double w = waves(kWideLanes, n - start);
+      const double need = (pre[n] - pre[start]) * work(kWideLanes, w > 1.5 * free0);
+      *work_out += need;
+      std::sort(fin, fin + nf);
+      double done = 0, tw = -1, t_prev = 0, rate = free0;
+      for (int i = 0; i <= nf && tw < 0; ++i) {
+        const double t_end = i < nf ? fin[i].first : 1e300;
+        const double cap = (t_end - t_prev) * rate;
+        if (done + cap >= need) tw = t_prev + (need - done) / rate;
+        done += cap;
+        t_prev = t_end;
+        if (i < nf) rate += 4.0 * fin[i].second;
+      }
+      // the longest WIDE job runs alone on its SIMD only if every WIDE wave has one
+      const double stretch = w > free0 ? 2.0 / kWideShare : 1.0;
+      t = std::max(t, std::max(tw, blocks(start) * 740.0 * kCpiWideBusy * stretch));
+    }
+    return t;
+  };
+  // equal makespans (within 2 %): prefer less issue work (fewer busy SIMDs, higher clock)
+  Part best[EFES_PLAN_MAX_PARTS - 1] = {};
+  int best_k = 0;
+  double best_t = -1, best_work = 0;
+  auto consider = [&](const Part* ps, int k) {
+    double wk = 0;
+    const double t = evaluate(ps, k, &wk);
+    if (t < 0) return;
+    if (best_t < 0 || t < best_t * 0.98 || (t < best_t * 1.02 && wk < best_work)) {
+      std::copy(ps, ps + k, best);
+      best_k = k;
+      best_t = t;
+      best_work = wk;
+    }
+  };
+  for (size_t a = 0; a < cuts.size(); ++a) {  // two exclusive parts (either may be empty)
     for (int g0 : shapes) {
-      if (g0 == kWideLanes || (d1 == 0 && g0 != 64)) continue;
-      double cus0 = 0;
-      const double t0 = d1 ? deep_time(g0, 0, d1, &cus0) : 0.0;
-      for (size_t b = a; b < cuts.size(); ++b) {
-        const uint32_t d2 = cuts[b];
+      if (g0 == kWideLanes || (cuts[a] == 0 && g0 != 64)) continue;
+      for (size_t b = a; b < cuts.size(); ++b)
         for (int g1 : shapes) {
-          if (d2 == d1 && g1 != 64) continue;
-          double cus1 = 0;
-          const double t1 = d2 > d1 ? deep_time(g1, d1, d2 - d1, &cus1) : 0.0;
-          const bool wide = d2 < n;
-          if ((d1 && d2 > d1 && cus0 + cus1 > cus) || (wide && cus0 + cus1 >= cus)) continue;
-          double t = std::max(t0, t1);
-          double wk = pre[d1] * work(g0, false) + (pre[d2] - pre[d1]) * work(g1, false);
-          if (wide) {
-            // WIDE work drains through the free SIMDs: 4*(cus - cus0 - cus1) until the shorter
-            // deep part ends, then its CUs join, then the other's.
-            const double free0 = 4.0 * (cus - cus0 - cus1);
-            const double w = waves(kWideLanes, n - d2);
-            const double need = (pre[n] - pre[d2]) * work(kWideLanes, w > 1.5 * free0);
-            wk += need;
-            double ta = d1 ? t0 : 0.0, tb = d2 > d1 ? t1 : 0.0, ca = cus0, cb = cus1;
-            if (ta > tb) { std::swap(ta, tb); std::swap(ca, cb); }
-            double done = 0, tw = 0;
-            const double seg[3][2] = {{ta, free0}, {tb, free0 + 4.0 * ca}, {1e300, 4.0 * cus}};
-            double t_prev = 0;
-            for (const auto& sg : seg) {
-              const double cap = (sg[0] - t_prev) * sg[1];
-              if (done + cap >= need) { tw = t_prev + (need - done) / sg[1]; break; }
-              done += cap;
-              t_prev = sg[0];
-            }
-            // the longest WIDE job runs alone on its SIMD only if every WIDE wave has one
-            const double stretch = w > free0 ? 2.0 / kWideShare : 1.0;
-            t = std::max(t, std::max(tw, blocks(d2) * latency(kWideLanes) * stretch));
-          }
-          // equal makespans (within 2 %): prefer less issue work (fewer busy SIMDs, higher clock)
-          if (best.t < 0 || t < best.t * 0.98 || (t < best.t * 1.02 && wk < best_work)) {
-            if (best.t < 0 || t < best.t * 1.02) {
-              best = Cand{t, d1, d2, g0, g1};
-              best_work = wk;
-            }
-          }
+          if (cuts[b] == cuts[a] && g1 != 64) continue;
+          const Part ps[2] = {{cuts[a], g0}, {cuts[b], g1}};
+          consider(ps, 2);
         }
+    }
+  }
+  if (best_k == 2 && best[1].end > best[0].end && best[1].end < n) {  // a third one after the best two
+    const Part two[2] = {best[0], best[1]};
+    for (uint32_t d3 : cuts) {
+      if (d3 <= two[1].end) continue;
+      for (int g2 : shapes) {
+        const Part ps[3] = {two[0], two[1], {d3, g2}};
+        consider(ps, 3);
       }
     }
   }
 
   efes_plan_part parts[EFES_PLAN_MAX_PARTS] = {};
-  uint32_t np = 0;
-  if (best.d1) parts[np++] = efes_plan_part{best.d1, mode_of(best.g0), 1u, 0u};
-  if (best.d2 > best.d1) parts[np++] = efes_plan_part{best.d2 - best.d1, mode_of(best.g1), 1u, 0u};
-  if (n > best.d2) parts[np++] = efes_plan_part{n - best.d2, EFES_MODE_WIDE, 0u, 0u};
+  uint32_t np = 0, prev = 0;
+  for (int i = 0; i < best_k; ++i) {
+    if (best[i].end > prev) parts[np++] = efes_plan_part{best[i].end - prev, mode_of(best[i].g), 1u, 0u};
+    prev = std::max(prev, best[i].end);
+  }
+  if (n > prev) parts[np++] = efes_plan_part{n - prev, EFES_MODE_WIDE, 0u, 0u};
 
   // Developer override for calibration runs:
   //   EFES_PLAN_FORCE="<lanes>:<jobs>[x],<lanes>:<jobs>[x],..."  (lanes 64 = DEEP, 0 = WIDE,
-  //   1 = FED4, 2 = FED4E (both always exclusive), x = exclusive); jobs beyond the listed parts run WIDE (a fourth
-  //   part is not possible).
+  //   1 = FED4, 2 = FED4E (both always exclusive), x = exclusive); jobs beyond the listed parts run
+  //   WIDE (a part beyond EFES_PLAN_MAX_PARTS is not possible).
   if (const char* f = getenv("EFES_PLAN_FORCE"); f && *f) {
     efes_plan_part fp[EFES_PLAN_MAX_PARTS] = {};
     uint32_t fn = 0, used = 0;
@@ -231,9 +265,11 @@ int efes_plan_batch(efes_ctx* ctx, const uint64_t* lengths, uint32_t n, uint32_t
   }
   plan->nparts = np;
   std::copy(parts, parts + np, plan->part);
-  plan->est_seconds = best.t / kClock;
+  plan->est_seconds = best_t / kClock;
   return EFES_OK;
 }
+
+static int hip_err_plan(hipError_t e) { return e == hipSuccess ? EFES_OK : EFES_ERR_HIP; }
 
 int efes_hash_submit_plan(efes_ctx* ctx, const efes_job* jobs, const efes_plan* plan, void* stream) {
   if (!ctx || !plan || plan->nparts > EFES_PLAN_MAX_PARTS || (plan->njobs && !jobs) || plan->njobs > EFES_MAX_JOBS)
@@ -257,18 +293,23 @@ int efes_hash_submit_plan(efes_ctx* ctx, const efes_job* jobs, const efes_plan* 
     return efes::launch_group(first, p.jobs, lanes_of(p.mode), ctx->d_tabs, st, p.exclusive != 0);
   };
   std::lock_guard<std::mutex> lk(ctx->plan_mu);
-  // Fork: parts 0..k-2 on side streams (longest jobs first, so their workgroups are placed
-  // first), the last part on `stream`; join: `stream` waits for every side stream.
-  hipError_t e = plan->nparts > 1 ? hipEventRecord(ctx->ev_fork, s) : hipSuccess;
+  // Fork: part i on the context's part stream i (longest jobs first, so their workgroups are
+  // placed first); join: `stream` waits for every part.  The part streams were created one after
+  // the other with the context, so they sit on distinct hardware queues (GPU_MAX_HW_QUEUES is 4):
+  // a part launched on the caller's stream instead could share a hardware queue with another
+  // part and not start before that one ends (seen in kernel traces: profiles/r02_mixtrace/).
+  if (plan->nparts == 1) return hip_err_plan(launch(plan->part[0], jobs, s));
+  hipError_t e = hipEventRecord(ctx->ev_fork, s);
   const efes_job* first = jobs;
-  for (uint32_t i = 0; i + 1 < plan->nparts && e == hipSuccess; ++i) {
-    e = hipStreamWaitEvent(ctx->side[i], ctx->ev_fork, 0);
-    if (e == hipSuccess) e = launch(plan->part[i], first, ctx->side[i]);
-    if (e == hipSuccess) e = hipEventRecord(ctx->ev_join[i], ctx->side[i]);
+  for (uint32_t i = 0; i < plan->nparts && e == hipSuccess; ++i) {
+    hipStream_t ps = ctx->part_stream(i);
+    if (ps != s) e = hipStreamWaitEvent(ps, ctx->ev_fork, 0);
+    if (e == hipSuccess) e = launch(plan->part[i], first, ps);
+    if (e == hipSuccess && ps != s) e = hipEventRecord(ctx->ev_join[i], ps);
     first += plan->part[i].jobs;
   }
-  if (e == hipSuccess) e = launch(plan->part[plan->nparts - 1], first, s);
-  for (uint32_t i = 0; i + 1 < plan->nparts && e == hipSuccess; ++i) e = hipStreamWaitEvent(s, ctx->ev_join[i], 0);
+  for (uint32_t i = 0; i < plan->nparts && e == hipSuccess; ++i)
+    if (ctx->part_stream(i) != s) e = hipStreamWaitEvent(s, ctx->ev_join[i], 0);
   return e == hipSuccess ? EFES_OK : EFES_ERR_HIP;
 }
 

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define EFES_ABI_VERSION 1
+#define EFES_ABI_VERSION 2
 
 /* ---- error codes ---------------------------------------------------------------- */
 #define EFES_OK 0
@@ -146,10 +146,10 @@ int efes_auto_mode(const efes_ctx* ctx, uint32_t njobs);
  * efes_plan_batch orders the jobs longest-first (order[i] = index into `lengths` of the job to
  * place at jobs_device[i]) and picks the cuts, shapes and exclusivity from an issue-time model
  * of the kernels calibrated on MI355X; efes_hash_submit_plan launches a batch
- * laid out in that order: every part but the last on a side stream of the context, the last on
- * `stream`, which then waits for all of them.  Planning is host-only (no device access; ctx
+ * laid out in that order: each part on a stream of the context (distinct hardware queues), after
+ * the work queued on `stream`, which then waits for all of them.  Planning is host-only (no device access; ctx
  * may be NULL: then the capacity of one MI355X, 256 CUs, is assumed). */
-#define EFES_PLAN_MAX_PARTS 3
+#define EFES_PLAN_MAX_PARTS 4
 typedef struct efes_plan_part {
     uint32_t jobs;       /* consecutive jobs of this part (in plan order) */
     int32_t mode;        /* EFES_MODE_DEEP, EFES_MODE_GROUPn or EFES_MODE_WIDE */

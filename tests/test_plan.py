@@ -87,7 +87,7 @@ def test_force_override(monkeypatch, force, expect):
 def test_force_override_rejects_too_many_parts(monkeypatch):
     """A forced plan that would need a fourth part is ignored (the model's plan stands)."""
     _, model = plan_batch([MiB] * 3000)
-    monkeypatch.setenv("EFES_PLAN_FORCE", "4:10,8:10,16:10")
+    monkeypatch.setenv("EFES_PLAN_FORCE", "4:10,8:10,16:10,32:10")
     _, plan = plan_batch([MiB] * 3000)
     assert plan.parts() == model.parts()
 

@@ -83,6 +83,9 @@ def parse_args(argv=None):
     p.add_argument("--segment-bytes", type=int, default=256 << 10, help="host-inclusive pipeline segment")
     p.add_argument("--ingest-leg", choices=["auto", "on", "off"], default="auto",
                    help="also report BASELINE configs[4] per-GPU (auto = N=1 only)")
+    p.add_argument("--uploads-leg", choices=["auto", "on", "off"], default="auto",
+                   help="also report the server path (tools/bench_uploads: 32 request threads x 256 uploads in "
+                        "flight, 8192 x 4 MiB, 32 KiB pageable Writes, Sum each); auto = N=1 only")
     p.add_argument("--concurrency-leg", choices=["auto", "on", "off"], default="auto",
                    help="also report 4 MiB chunks at 1K..192K in flight, one AUTO launch each (auto = N=1 only)")
     p.add_argument("--mixed-leg", choices=["auto", "on", "off"], default="auto",
@@ -543,6 +546,10 @@ def main(argv=None):
                                                    batches[0])
         if args.ingest_leg == "on" or (args.ingest_leg == "auto" and world == 1):
             out["ingest_config"] = ingest_leg(args, rank, world, ctx, device, stream, MODE_AUTO)
+        if args.uploads_leg == "on" or (args.uploads_leg == "auto" and world == 1):
+            a = argparse.Namespace(**vars(args))
+            a.upload_threads, a.uploads, a.open_per_thread, a.upload_bytes = 32, 8192, 256, 4 << 20
+            out["uploads_path"] = uploads_workload(a, ctx)
         if args.concurrency_leg == "on" or (args.concurrency_leg == "auto" and world == 1):
             out["concurrency"] = concurrency_leg(args, ctx, device, stream)
         if args.mixed_leg == "on" or (args.mixed_leg == "auto" and world == 1):

@@ -640,7 +640,7 @@ def test_bench_emits_driver_json(env):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--chunks", "16", "--chunk-bytes", "65536",
                           "--steps", "2", "--warmup", "1", "--cpu-seconds", "0.1", "--segment-bytes", "16384",
-                          "--mixed-leg", "off"],
+                          "--mixed-leg", "off", "--uploads-leg", "off"],
                          capture_output=True, text=True, timeout=600, check=True).stdout
     d = json.loads(out.strip().splitlines()[-1])
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",

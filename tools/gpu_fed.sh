@@ -7,6 +7,6 @@ rc=$?; tail -5 gpurun_out/fed/tests.log; [ $rc -eq 0 ] || exit $rc
 for spec in "fed4 3072" "group4 3072" "fed4 12288" "group4 12288" "group4 16384" "fed4 6144"; do
   set -- $spec
   timeout -k 10 180 python bench.py --mode $1 --chunks $2 --steps 3 --warmup 1 --no-cpu-baseline --host-inclusive off \
-    --ingest-leg off --mixed-leg off --concurrency-leg off > gpurun_out/fed/$1_$2.json 2> gpurun_out/fed/$1_$2.err || { echo "FAIL $spec"; tail -5 gpurun_out/fed/$1_$2.err; exit 1; }
+    --ingest-leg off --mixed-leg off --concurrency-leg off --uploads-leg off > gpurun_out/fed/$1_$2.json 2> gpurun_out/fed/$1_$2.err || { echo "FAIL $spec"; tail -5 gpurun_out/fed/$1_$2.err; exit 1; }
   python3 -c "import json;d=json.load(open('gpurun_out/fed/$1_$2.json'));print('$1 $2', d['value'], 'GiB/s', d['roofline']['kernel_ms'], 'ms')"
 done

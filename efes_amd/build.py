@@ -61,6 +61,38 @@ def build_tools() -> list[str]:
     return out
 
 
+RECEIVER_SRC = os.path.join(HERE, "host", "efes_receiver.cpp")
+RECEIVER_HDR = os.path.join(HERE, "host", "efes_receiver.hpp")
+RECEIVER_LIB = os.path.join(LIB_DIR, "libefesreceiver.so")
+
+
+def build_receiver(force: bool = False) -> str:
+    """libefesreceiver.so: the C++ mirror of the Go callers above the C ABI (fileinfo.go,
+    filereceiver.go, sha1file.go), linked against libefeshash.so."""
+    deps = [RECEIVER_SRC, RECEIVER_HDR, LIB, os.path.join(ROOT, "include", "efes_hash.h")]
+    if force or _stale(RECEIVER_LIB, deps):
+        tmp = RECEIVER_LIB + ".tmp"
+        subprocess.run(["g++", "-O2", "-std=c++17", "-Wall", "-Wextra", "-fPIC", "-shared", "-pthread",
+                        "-I", os.path.join(ROOT, "include"), RECEIVER_SRC, "-o", tmp,
+                        "-L", LIB_DIR, "-lefeshash", "-Wl,-rpath,$ORIGIN"], check=True)
+        os.replace(tmp, RECEIVER_LIB)
+    return RECEIVER_LIB
+
+
+def build_receiver_test() -> str:
+    """tests/cpp/receiver_test: the reference's receiver / Sha1File tests replayed against the C++
+    mirror, checked against the oracle (test infrastructure)."""
+    src = os.path.join(ROOT, "tests", "cpp", "receiver_test.cpp")
+    exe = os.path.join(ROOT, "tests", "cpp", "receiver_test")
+    oracle_lib = os.path.join(ROOT, "oracle", "liboracle.so")
+    if os.path.exists(src) and _stale(exe, [src, RECEIVER_LIB, RECEIVER_HDR, LIB, oracle_lib]):
+        subprocess.run(["g++", "-O2", "-std=c++17", "-Wall", "-Wextra", "-pthread", "-I", os.path.join(ROOT, "include"),
+                        src, "-o", exe, "-L", LIB_DIR, "-lefesreceiver", "-lefeshash",
+                        "-L", os.path.join(ROOT, "oracle"), "-loracle",
+                        "-Wl,-rpath,$ORIGIN/../../efes_amd/lib", "-Wl,-rpath,$ORIGIN/../../oracle"], check=True)
+    return exe
+
+
 def build_consumer_test() -> str:
     """tests/c/efes_consumer_test: a C consumer of the ABI checked against the oracle (test infrastructure)."""
     src = os.path.join(ROOT, "tests", "c", "efes_consumer_test.c")
@@ -84,3 +116,5 @@ if __name__ == "__main__":
     print(build_tools())
     print(build_oracle())
     print(build_consumer_test())
+    print(build_receiver())
+    print(build_receiver_test())

@@ -1,0 +1,38 @@
+"""The upload receiver above the C ABI (efes_amd/host/efes_receiver.hpp: the C++ mirror of
+fileinfo.go, filereceiver.go and sha1file.go) driven by the reference's own tests, replayed in
+tests/cpp/receiver_test.cpp with every digest and every `.info` byte checked against the oracle.
+
+cpu: the `.info` JSON codec (json.Encoder / Decoder semantics), strconv / filepath helpers, and
+     the handler paths that end before any hashing (POST, HEAD, DELETE, 400, 409).
+gpu: filereceiver_test.go's six tests with the digest headers asserted (KATs for "foo", "baz",
+     "foobar", ""), sha1file_test.go over a real file, 16 threads of resumable uploads through
+     ServeHTTP, and saveFile's error paths (broken body, vanished file, Go panic states)."""
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EXE = os.path.join(ROOT, "tests", "cpp", "receiver_test")
+
+
+def _run(args, timeout):
+    if not os.path.exists(EXE):
+        pytest.fail(f"{EXE} not built (__graft_entry__.build())")
+    return subprocess.run([EXE] + args, capture_output=True, text=True, timeout=timeout)
+
+
+def test_receiver_cpu(tmp_path):
+    r = _run(["cpu", str(tmp_path)], 60)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "receiver_test cpu ok" in r.stdout, r.stdout
+
+
+@pytest.mark.gpu
+def test_receiver_gpu(tmp_path):
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    r = _run(["gpu", str(tmp_path), "16", "4"], 110)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "receiver_test gpu ok" in r.stdout, r.stdout

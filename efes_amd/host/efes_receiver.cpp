@@ -638,12 +638,15 @@ struct FdGuard {
 };
 }  // namespace
 
-Error saveFile(Hasher& h, const std::string& path, int64_t offset, int64_t length, Reader& r, int64_t* new_offset,
+Error saveFile(Hasher* h, const std::string& path, int64_t offset, int64_t length, Reader& r, int64_t* new_offset,
                bool* done, DigestSums* sums) {  // filereceiver.go:171-227
   *new_offset = 0;
   *done = false;
   FileInfo fi;
+  // A receiver without a GPU context (h == nullptr) fails every request that would hash, before
+  // touching the file: there is no CPU fallback.  Offset mismatches are still reported first.
   if (offset == 0) {
+    if (!h) return lib_error(EFES_ERR_NO_DEVICE);
     Error e = createFile(path);  // a PATCH at 0 needs no prior POST (filereceiver.go:175)
     if (e) return e;
     fi = newFileInfo();
@@ -651,6 +654,7 @@ Error saveFile(Hasher& h, const std::string& path, int64_t offset, int64_t lengt
     Error e = ReadFileInfo(path, &fi);
     if (e) return e;
     if (offset != fi.Offset) return offset_mismatch(offset, fi.Offset);
+    if (!h) return lib_error(EFES_ERR_NO_DEVICE);
   }
   FdGuard f;
   f.fd = ::open(path.c_str(), O_WRONLY | O_CLOEXEC);  // os.OpenFile(path, os.O_WRONLY, 0600)
@@ -666,10 +670,10 @@ Error saveFile(Hasher& h, const std::string& path, int64_t offset, int64_t lengt
   // w := io.MultiWriter(f, fi.Digest.CRC32, fi.Digest.Sha1) (filereceiver.go:208).  Go would
   // panic writing into a nil digest; refuse the request instead.
   if (!fi.has_sha1 || !fi.has_crc32) return make_error(ERR_NIL_DIGEST, "nil digest in " + path + fileInfoExt);
-  UploadGuard g(h);
-  h.acquire();
+  UploadGuard g(*h);
+  h->acquire();
   g.held = true;
-  int rc = efes_upload_open(h.queue(), EFES_HASH_SHA1 | EFES_HASH_CRC32, &fi.Sha1, &fi.CRC32, &g.u);
+  int rc = efes_upload_open(h->queue(), EFES_HASH_SHA1 | EFES_HASH_CRC32, &fi.Sha1, &fi.CRC32, &g.u);
   if (rc) return lib_error(rc);
 
   // n, _ := io.Copy(w, r) (filereceiver.go:209): 32 KiB buffers; a read error ends the copy
@@ -827,7 +831,7 @@ Response FileReceiver::ServeHTTP(const Request& r) {  // filereceiver.go:42-127
     int64_t new_offset = 0;
     bool done = false;
     DigestSums sums;
-    Error e = saveFile(*h_, path, offset, length, body, &new_offset, &done, &sums);
+    Error e = saveFile(h_, path, offset, length, body, &new_offset, &done, &sums);
     if (e.code == ERR_OFFSET_MISMATCH) {  // filereceiver.go:85-93
       w.Headers["Content-Type"] = "text/plain; charset=utf-8";
       w.Headers["X-Content-Type-Options"] = "nosniff";

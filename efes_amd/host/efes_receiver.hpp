@@ -139,7 +139,8 @@ class Hasher {
 Error createFile(const std::string& path);                 // filereceiver.go:148-165
 Error deleteFile(const std::string& path);                 // filereceiver.go:167-169
 // filereceiver.go:171-227: returns the new offset; *done (with *sums) when offset == length.
-Error saveFile(Hasher& h, const std::string& path, int64_t offset, int64_t length, Reader& r,
+// h == nullptr (no GPU context): every request that gets as far as hashing fails.
+Error saveFile(Hasher* h, const std::string& path, int64_t offset, int64_t length, Reader& r,
                int64_t* new_offset, bool* done, DigestSums* sums);
 std::string OffsetMismatchText(int64_t given, int64_t required);  // OffsetMismatchError.Error()
 

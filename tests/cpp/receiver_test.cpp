@@ -312,6 +312,10 @@ static void test_handler_cpu(const std::string& root) {
   w = c.send(3, -1, "x");
   CHECK(w.Code == 500 && w.Body == "cannot save file: invalid digest\n", "corrupt .info PATCH: %d %s", w.Code,
         w.Body.c_str());
+  // no GPU context behind the receiver: a PATCH that reaches saveFile fails loudly (no CPU fallback)
+  w = c.send(0, -1, "x");
+  CHECK(w.Code == 500 && w.Body == "cannot save file: no usable gfx950 device\n", "no hasher: %d %s", w.Code,
+        w.Body.c_str());
 }
 
 // =================================================================================================

@@ -21,6 +21,7 @@ Printed on rank 0: ONE JSON line with the driver's keys plus
 from __future__ import annotations
 
 import argparse
+import functools
 import glob
 import json
 import os
@@ -86,6 +87,9 @@ def parse_args(argv=None):
     p.add_argument("--uploads-leg", choices=["auto", "on", "off"], default="auto",
                    help="also report the server path (tools/bench_uploads: 32 request threads x 256 uploads in "
                         "flight, 8192 x 4 MiB, 32 KiB pageable Writes, Sum each); auto = N=1 only")
+    p.add_argument("--receiver-leg", choices=["auto", "on", "off"], default="auto",
+                   help="also report the receiver with files (tools/bench_receiver: saveFile through ServeHTTP, "
+                        "1024 request threads x 4 MiB PATCHes on tmpfs) and Sha1File read-back; auto = N=1 only")
     p.add_argument("--concurrency-leg", choices=["auto", "on", "off"], default="auto",
                    help="also report 4 MiB chunks at 1K..192K in flight, one AUTO launch each (auto = N=1 only)")
     p.add_argument("--mixed-leg", choices=["auto", "on", "off"], default="auto",
@@ -199,6 +203,7 @@ def host_inclusive(ctx, data, n: int, chunk: int, do_crc: bool, segment: int, ba
                     "zero_copy_value = one DEEP launch reading the pinned chunks over PCIe in place; not `value`"}
 
 
+@functools.lru_cache(maxsize=2)
 def _xorshift_bytes(n: int) -> bytes:
     """The byte stream tools/bench_uploads.cpp hashes (xorshift64, low byte of each step)."""
     out = bytearray(n)
@@ -231,6 +236,35 @@ def uploads_workload(args, ctx):
     res["digests_match"] = res.pop("sum_sha1_crc32") == want and res.pop("all_sums_equal")
     res["note"] = "native request threads: pageable Writes -> pinned staging -> batched launches -> per-upload Sum"
     return res
+
+
+def receiver_leg():
+    """The Go callers above the ABI, restated in C++ (efes_amd/host/efes_receiver.hpp), driven by
+    tools/bench_receiver: request threads run saveFile through FileReceiver::ServeHTTP (file write,
+    fsync, the fused upload, .info between PATCHes, digest headers at the end; one PATCH at a time
+    per thread, as net/http runs a handler), files on tmpfs when there is one; and Sha1File over a
+    file (write.go:69).  Digests checked against hashlib/zlib.  Returns the result dict."""
+    import hashlib
+    import subprocess
+    import tempfile
+    import zlib
+
+    exe = os.path.join(ROOT, "tools", "bench_receiver")
+    base = "/dev/shm" if os.access("/dev/shm", os.W_OK) else tempfile.gettempdir()
+    out = {}
+    with tempfile.TemporaryDirectory(dir=base, prefix="efes_receiver_") as d:
+        for key, argv, size in (("receiver", ["receiver", d, "1024", "2", str(4 << 20), str(4 << 20)], 4 << 20),
+                                ("sha1file", ["sha1file", d, "64", "8", str(4 << 20)], 4 << 20)):
+            r = subprocess.run([exe] + argv, check=True, capture_output=True, text=True, timeout=300)
+            res = json.loads(r.stdout.strip().splitlines()[-1])
+            src = _xorshift_bytes(size)
+            want = hashlib.sha1(src).hexdigest() + ("%08x" % zlib.crc32(src) if key == "receiver" else "")
+            got = res.pop("sum_sha1_crc32" if key == "receiver" else "sum_sha1")
+            res["digests_match"] = got == want and res.pop("all_sums_equal")
+            out[key] = res
+    out["note"] = ("host-CPU bound (file writes, staging copies, syscalls of 1024 request threads); "
+                   "not `value`")
+    return out
 
 
 def make_workload(args, rank: int, world: int, ctx, device: str, stream):
@@ -550,6 +584,8 @@ def main(argv=None):
             a = argparse.Namespace(**vars(args))
             a.upload_threads, a.uploads, a.open_per_thread, a.upload_bytes = 32, 8192, 256, 4 << 20
             out["uploads_path"] = uploads_workload(a, ctx)
+        if args.receiver_leg == "on" or (args.receiver_leg == "auto" and world == 1):
+            out["receiver_path"] = receiver_leg()
         if args.concurrency_leg == "on" or (args.concurrency_leg == "auto" and world == 1):
             out["concurrency"] = concurrency_leg(args, ctx, device, stream)
         if args.mixed_leg == "on" or (args.mixed_leg == "auto" and world == 1):

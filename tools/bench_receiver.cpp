@@ -1,0 +1,209 @@
+// Native driver for the upload receiver above the C ABI (efes_amd/host/efes_receiver.hpp): the
+// storage server's PATCH path end to end -- file write, fsync, the fused SHA-1 + CRC-32 on the
+// GPU, the .info state between PATCHes and the digest headers of the last one -- with T threads
+// standing in for the request goroutines of server.go:130 (one PATCH at a time each, as net/http
+// runs a handler), and the read-back path (Sha1File over files, write.go:69 / drain.go:125).
+// Prints one JSON line per mode.  Not part of the product library.
+//
+//   tools/bench_receiver receiver <dir> <threads> <uploads_per_thread> <upload_bytes> <patch_bytes>
+//   tools/bench_receiver sha1file <dir> <threads> <files_per_thread> <file_bytes>
+//
+// Every upload carries the same bytes, so every finished upload must report the digests of a
+// reference upload made before the clock starts; each file is removed when its upload is done
+// (the store keeps it; the benchmark bounds the space it needs to threads x upload_bytes).
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/statfs.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../efes_amd/host/efes_receiver.hpp"
+
+using namespace efes;
+
+namespace {
+
+// An io.Reader over caller memory, at most `max_read` bytes per Read (a socket's reads).
+struct SpanReader : Reader {
+  const uint8_t* p;
+  size_t n, pos = 0, max_read;
+  SpanReader(const uint8_t* d, size_t len, size_t mr) : p(d), n(len), max_read(mr) {}
+  size_t Read(uint8_t* dst, size_t cap, Error* err) override {
+    *err = Error{};
+    if (pos >= n) {
+      *err = make_error(ERR_EOF, "EOF");
+      return 0;
+    }
+    const size_t k = std::min(std::min(cap, max_read), n - pos);
+    memcpy(dst, p + pos, k);
+    pos += k;
+    return k;
+  }
+};
+
+std::vector<uint8_t> content(size_t n) {
+  std::vector<uint8_t> v(n);
+  uint64_t z = 0x9E3779B97F4A7C15ull;
+  for (size_t i = 0; i < n; ++i) {
+    z ^= z << 13; z ^= z >> 7; z ^= z << 17;
+    v[i] = (uint8_t)z;
+  }
+  return v;
+}
+
+const char* fs_name(const std::string& dir) {
+  struct statfs s;
+  if (statfs(dir.c_str(), &s) != 0) return "unknown";
+  return s.f_type == 0x01021994 ? "tmpfs" : "disk";
+}
+
+// One upload through ServeHTTP, PATCH by PATCH; returns the final response.
+Response upload(FileReceiver& fr, const std::string& path, const std::vector<uint8_t>& src, size_t patch) {
+  Response w;
+  size_t off = 0;
+  do {
+    const size_t n = std::min(patch, src.size() - off);
+    SpanReader body(src.data() + off, n, 32 << 10);
+    Request r;
+    r.Method = "PATCH";
+    r.Path = path;
+    r.Headers["efes-file-offset"] = std::to_string(off);
+    r.Headers["efes-file-length"] = std::to_string(src.size());
+    r.Body = &body;
+    w = fr.ServeHTTP(r);
+    if (w.Code != 200) return w;
+    off += n;
+  } while (off < src.size());
+  return w;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  if (argc < 7 && !(argc >= 6 && std::string(argv[1]) == "sha1file")) {
+    fprintf(stderr,
+            "usage: %s receiver <dir> <threads> <uploads_per_thread> <upload_bytes> <patch_bytes>\n"
+            "       %s sha1file <dir> <threads> <files_per_thread> <file_bytes>\n",
+            argv[0], argv[0]);
+    return 2;
+  }
+  const std::string mode = argv[1], dir = argv[2];
+  const int T = atoi(argv[3]);
+  const long U = atol(argv[4]);
+  const size_t S = strtoull(argv[5], nullptr, 10);
+  efes_ctx* ctx = nullptr;
+  int rc = efes_ctx_create(0, &ctx);
+  if (rc) {
+    fprintf(stderr, "efes_ctx_create: %s\n", efes_strerror(rc));
+    return 1;
+  }
+  const std::vector<uint8_t> src = content(S);
+  std::atomic<int> bad{0}, errs{0};
+  double secs = 0;
+  std::string first;
+
+  if (mode == "receiver") {
+    const size_t P = strtoull(argv[6], nullptr, 10);
+    Hasher* h = nullptr;
+    Error e = Hasher::Create(ctx, 256 << 10, 4u * (uint32_t)T + 64, (uint32_t)T, &h);
+    if (e) {
+      fprintf(stderr, "Hasher::Create: %s\n", e.msg.c_str());
+      return 1;
+    }
+    FileReceiver fr(dir, h);
+    {  // the expected headers, from one upload before the clock
+      Response w = upload(fr, "/bench/reference.fid", src, P);
+      first = w.Headers["efes-file-sha1"] + w.Headers["efes-file-crc32"];
+      if (w.Code != 200 || first.size() != 48) {
+        fprintf(stderr, "reference upload: %d %s\n", w.Code, w.Body.c_str());
+        return 1;
+      }
+      (void)deleteFile(JoinPath(dir, "/bench/reference.fid"));
+    }
+    auto t0 = std::chrono::steady_clock::now();
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t)
+      th.emplace_back([&, t] {
+        for (long u = 0; u < U; ++u) {
+          const std::string path = "/bench/" + std::to_string(t) + "/" + std::to_string(u) + ".fid";
+          Response w = upload(fr, path, src, P);
+          if (w.Code != 200) {
+            ++errs;
+            fprintf(stderr, "%s: %d %s\n", path.c_str(), w.Code, w.Body.c_str());
+            return;
+          }
+          if (w.Headers["efes-file-sha1"] + w.Headers["efes-file-crc32"] != first) ++bad;
+          (void)deleteFile(JoinPath(dir, path));
+        }
+      });
+    for (auto& x : th) x.join();
+    secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    delete h;
+    printf("{\"workload\": \"receiver\", \"threads\": %d, \"uploads\": %ld, \"upload_bytes\": %zu, \"patch_bytes\": %zu, "
+           "\"read_bytes\": 32768, \"dir_fs\": \"%s\", \"seconds\": %.4f, \"value\": %.3f, \"unit\": \"GiB/s\", "
+           "\"sum_sha1_crc32\": \"%s\", \"all_sums_equal\": %s, \"errors\": %d}\n",
+           T, T * U, S, P, fs_name(dir), secs, (double)T * U * S / secs / (1u << 30), first.c_str(),
+           bad ? "false" : "true", errs.load());
+  } else if (mode == "sha1file") {
+    // One source file read by every thread U times through Sha1File (32 KiB reads).
+    const std::string path = dir + "/bench_sha1file.dat";
+    FILE* f = fopen(path.c_str(), "wb");
+    if (!f || fwrite(src.data(), 1, S, f) != S || fclose(f) != 0) {
+      fprintf(stderr, "cannot write %s\n", path.c_str());
+      return 1;
+    }
+    auto read_one = [&](std::string* hex) -> bool {
+      FileReader* fr = nullptr;
+      if (FileReader::Open(path, &fr)) return false;
+      Sha1File* sf = nullptr;
+      bool ok = !Sha1File::New(fr, ctx, &sf);
+      std::vector<uint8_t> buf(32 << 10);
+      Error e;
+      while (ok) {
+        sf->Read(buf.data(), buf.size(), &e);
+        if (e.code == ERR_EOF) break;
+        if (e) ok = false;
+      }
+      uint8_t d[20];
+      if (ok) ok = !sf->Sum(d);
+      if (ok) *hex = HexEncode(d, 20);
+      delete sf;
+      delete fr;
+      return ok;
+    };
+    if (!read_one(&first)) {
+      fprintf(stderr, "reference read failed\n");
+      return 1;
+    }
+    auto t0 = std::chrono::steady_clock::now();
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t)
+      th.emplace_back([&] {
+        for (long u = 0; u < U; ++u) {
+          std::string hx;
+          if (!read_one(&hx)) ++errs;
+          else if (hx != first) ++bad;
+        }
+      });
+    for (auto& x : th) x.join();
+    secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    unlink(path.c_str());
+    printf("{\"workload\": \"sha1file\", \"threads\": %d, \"files\": %ld, \"file_bytes\": %zu, \"read_bytes\": 32768, "
+           "\"dir_fs\": \"%s\", \"seconds\": %.4f, \"value\": %.3f, \"unit\": \"GiB/s\", \"sum_sha1\": \"%s\", "
+           "\"all_sums_equal\": %s, \"errors\": %d}\n",
+           T, T * U, S, fs_name(dir), secs, (double)T * U * S / secs / (1u << 30), first.c_str(), bad ? "false" : "true",
+           errs.load());
+  } else {
+    fprintf(stderr, "unknown mode %s\n", mode.c_str());
+    return 2;
+  }
+  efes_ctx_destroy(ctx);
+  return errs || bad ? 1 : 0;
+}

@@ -566,30 +566,53 @@ Error DeleteFileInfo(const std::string& path) { return remove_path(path + fileIn
 
 // ---- filereceiver.go ---------------------------------------------------------------------------
 Error Hasher::Create(efes_ctx* ctx, uint64_t chunk_bytes, uint32_t max_chunks, uint32_t max_uploads, Hasher** out) {
-  efes_queue* q = nullptr;
-  const int rc = efes_queue_create(ctx, chunk_bytes, max_chunks, max_uploads, &q);
-  if (rc) return lib_error(rc);
-  Hasher* h = new Hasher;
-  h->q_ = q;
-  h->free_ = max_uploads;
-  *out = h;
+  return Create(std::vector<efes_ctx*>{ctx}, chunk_bytes, max_chunks, max_uploads, out);
+}
+
+Error Hasher::Create(const std::vector<efes_ctx*>& ctxs, uint64_t chunk_bytes, uint32_t max_chunks,
+                     uint32_t max_uploads, Hasher** out) {
+  if (ctxs.empty()) return lib_error(EFES_ERR_ARG);
+  std::unique_ptr<Hasher> h(new Hasher);
+  for (efes_ctx* ctx : ctxs) {
+    efes_queue* q = nullptr;
+    const int rc = efes_queue_create(ctx, chunk_bytes, max_chunks, max_uploads, &q);
+    if (rc) return lib_error(rc);  // ~Hasher destroys the queues made so far
+    h->q_.push_back(q);
+    h->free_.push_back(max_uploads);
+    h->served_.push_back(0);
+  }
+  *out = h.release();
   return Error{};
 }
 
-Hasher::~Hasher() { efes_queue_destroy(q_); }
-
-void Hasher::acquire() {
-  std::unique_lock<std::mutex> lk(mu_);
-  cv_.wait(lk, [&] { return free_ > 0; });
-  --free_;
+Hasher::~Hasher() {
+  for (efes_queue* q : q_) efes_queue_destroy(q);
 }
 
-void Hasher::release() {
+size_t Hasher::acquire() {
+  std::unique_lock<std::mutex> lk(mu_);
+  size_t best = 0;
+  cv_.wait(lk, [&] {
+    for (size_t d = 0; d < free_.size(); ++d)  // most free slots; ties: the device that served fewer
+      if (free_[d] > free_[best] || (free_[d] == free_[best] && served_[d] < served_[best])) best = d;
+    return free_[best] > 0;
+  });
+  --free_[best];
+  ++served_[best];
+  return best;
+}
+
+void Hasher::release(size_t d) {
   {
     std::lock_guard<std::mutex> lk(mu_);
-    ++free_;
+    ++free_[d];
   }
   cv_.notify_one();
+}
+
+uint64_t Hasher::served(size_t d) const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return served_[d];
 }
 
 std::string OffsetMismatchText(int64_t given, int64_t required) {  // filereceiver.go:234-236
@@ -623,11 +646,12 @@ namespace {
 struct UploadGuard {
   Hasher& h;
   efes_upload* u = nullptr;
+  size_t dev = 0;
   bool held = false;
   explicit UploadGuard(Hasher& hh) : h(hh) {}
   ~UploadGuard() {
     if (u) efes_upload_close(u);
-    if (held) h.release();
+    if (held) h.release(dev);
   }
 };
 struct FdGuard {
@@ -671,9 +695,9 @@ Error saveFile(Hasher* h, const std::string& path, int64_t offset, int64_t lengt
   // panic writing into a nil digest; refuse the request instead.
   if (!fi.has_sha1 || !fi.has_crc32) return make_error(ERR_NIL_DIGEST, "nil digest in " + path + fileInfoExt);
   UploadGuard g(*h);
-  h->acquire();
+  g.dev = h->acquire();
   g.held = true;
-  int rc = efes_upload_open(h->queue(), EFES_HASH_SHA1 | EFES_HASH_CRC32, &fi.Sha1, &fi.CRC32, &g.u);
+  int rc = efes_upload_open(h->queue(g.dev), EFES_HASH_SHA1 | EFES_HASH_CRC32, &fi.Sha1, &fi.CRC32, &g.u);
   if (rc) return lib_error(rc);
 
   // n, _ := io.Copy(w, r) (filereceiver.go:209): 32 KiB buffers; a read error ends the copy

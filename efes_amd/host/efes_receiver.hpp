@@ -29,6 +29,7 @@
 #include <mutex>
 #include <string>
 #include <string_view>
+#include <vector>
 
 #include "efes_hash.h"
 
@@ -118,22 +119,29 @@ struct DigestSums {
   uint8_t crc32[4];
 };
 
-// A hashing backend for saveFile: one batching queue shared by every request of a process
-// (the role of the per-request digests of the reference, batched).  max_uploads bounds the
-// requests hashed at once; further requests wait for a slot.
+// A hashing backend for saveFile: one batching queue per GPU, shared by every request of the
+// process (the role of the per-request digests of the reference, batched).  Each PATCH is hashed
+// on the device with the most free request slots (the state travels through the .info file
+// between PATCHes, so consecutive PATCHes of one upload may use different GPUs); max_uploads
+// bounds the requests hashed at once per device, further requests wait for a slot.
 class Hasher {
  public:
   static Error Create(efes_ctx* ctx, uint64_t chunk_bytes, uint32_t max_chunks, uint32_t max_uploads, Hasher** out);
+  static Error Create(const std::vector<efes_ctx*>& ctxs, uint64_t chunk_bytes, uint32_t max_chunks,
+                      uint32_t max_uploads, Hasher** out);  // one queue per context (GPU)
   ~Hasher();
-  efes_queue* queue() const { return q_; }
-  void acquire();
-  void release();
+  size_t devices() const { return q_.size(); }
+  efes_queue* queue(size_t d = 0) const { return q_[d]; }
+  size_t acquire();          // a request slot on the least-loaded device (blocks while all are busy)
+  void release(size_t d);
+  uint64_t served(size_t d) const;  // requests hashed on device d so far
 
  private:
-  efes_queue* q_ = nullptr;
-  std::mutex mu_;
+  std::vector<efes_queue*> q_;
+  std::vector<uint32_t> free_;
+  std::vector<uint64_t> served_;
+  mutable std::mutex mu_;
   std::condition_variable cv_;
-  uint32_t free_ = 0;
 };
 
 Error createFile(const std::string& path);                 // filereceiver.go:148-165

@@ -570,8 +570,8 @@ static uint64_t rnd(uint64_t* s) {
   return *s * 0x2545F4914F6CDD1Dull;
 }
 
-static void upload_worker(const std::string& dir, int uploads, Up* a) {
-  FileReceiver fr(dir, g_hasher);
+static void upload_worker(const std::string& dir, int uploads, Up* a, Hasher* hasher) {
+  FileReceiver fr(dir, hasher);
   uint64_t s = 0x9E3779B97F4A7C15ull ^ (uint64_t)(a->id + 1) * 0xD1B54A32D192ED03ull;
   for (int u = 0; u < uploads && !g_fail; ++u) {
     Client c{&fr};
@@ -620,13 +620,14 @@ static void upload_worker(const std::string& dir, int uploads, Up* a) {
   }
 }
 
-static void test_concurrent_uploads(const std::string& root, int threads, int uploads) {
-  const std::string dir = fresh_dir(root, "uploads");
+static void test_concurrent_uploads(const std::string& root, int threads, int uploads, Hasher* hasher,
+                                    const char* name) {
+  const std::string dir = fresh_dir(root, name);
   std::vector<Up> args(threads);
   std::vector<std::thread> th;
   for (int t = 0; t < threads; ++t) {
     args[t].id = t;
-    th.emplace_back(upload_worker, dir, uploads, &args[t]);
+    th.emplace_back(upload_worker, dir, uploads, &args[t], hasher);
   }
   long patches = 0, bytes = 0;
   for (int t = 0; t < threads; ++t) {
@@ -634,7 +635,10 @@ static void test_concurrent_uploads(const std::string& root, int threads, int up
     patches += args[t].patches;
     bytes += args[t].bytes;
   }
-  printf("uploads: %d threads x %d uploads, %ld PATCHes, %ld bytes\n", threads, uploads, patches, bytes);
+  printf("%s: %d threads x %d uploads, %ld PATCHes, %ld bytes, PATCHes per device:", name, threads, uploads, patches,
+         bytes);
+  for (size_t d = 0; d < hasher->devices(); ++d) printf(" %llu", (unsigned long long)hasher->served(d));
+  printf("\n");
 }
 
 int main(int argc, char** argv) {
@@ -667,8 +671,24 @@ int main(int argc, char** argv) {
     test_file_receiver(root);
     if (!g_fail) test_save_file_errors(root);
     if (!g_fail) test_sha1file(root);
-    if (!g_fail) test_concurrent_uploads(root, threads, uploads);
+    if (!g_fail) test_concurrent_uploads(root, threads, uploads, g_hasher, "uploads");
     delete g_hasher;
+    // Several GPUs in one process: one queue per context, each PATCH on the least-loaded one
+    // (two contexts on device 0 stand in for two GPUs on a one-GPU box).
+    efes_ctx* ctx2 = nullptr;
+    if (!g_fail && (rc = efes_ctx_create(0, &ctx2)) == 0) {
+      Hasher* multi = nullptr;
+      Error me = Hasher::Create(std::vector<efes_ctx*>{g_ctx, ctx2}, 256 << 10, 512, 32, &multi);
+      CHECK(!me, "multi-device Hasher: %s", me.msg.c_str());
+      if (multi) {
+        test_concurrent_uploads(root, threads, uploads, multi, "uploads over 2 queues");
+        CHECK(multi->served(0) > 0 && multi->served(1) > 0, "both devices served PATCHes");
+        delete multi;
+      }
+      efes_ctx_destroy(ctx2);
+    } else if (!g_fail) {
+      CHECK(false, "second context: %s", efes_strerror(rc));
+    }
     efes_ctx_destroy(g_ctx);
   } else {
     fprintf(stderr, "unknown mode %s\n", mode.c_str());

@@ -5,7 +5,9 @@
 // runs a handler), and the read-back path (Sha1File over files, write.go:69 / drain.go:125).
 // Prints one JSON line per mode.  Not part of the product library.
 //
-//   tools/bench_receiver receiver <dir> <threads> <uploads_per_thread> <upload_bytes> <patch_bytes>
+//   tools/bench_receiver receiver <dir> <threads> <uploads_per_thread> <upload_bytes> <patch_bytes> [gpus]
+//                                 (gpus > 1: one process over several GPUs, a queue per GPU, each
+//                                  PATCH on the least-loaded one -- a storage server is one process)
 //   tools/bench_receiver sha1file <dir> <threads> <files_per_thread> <file_bytes>
 //
 // Every upload carries the same bytes, so every finished upload must report the digests of a
@@ -111,8 +113,18 @@ int main(int argc, char** argv) {
 
   if (mode == "receiver") {
     const size_t P = strtoull(argv[6], nullptr, 10);
+    const int G = argc > 7 ? atoi(argv[7]) : 1;
+    std::vector<efes_ctx*> ctxs{ctx};
+    for (int g = 1; g < G; ++g) {
+      efes_ctx* c = nullptr;
+      if ((rc = efes_ctx_create(g, &c))) {
+        fprintf(stderr, "efes_ctx_create(%d): %s\n", g, efes_strerror(rc));
+        return 1;
+      }
+      ctxs.push_back(c);
+    }
     Hasher* h = nullptr;
-    Error e = Hasher::Create(ctx, 256 << 10, 4u * (uint32_t)T + 64, (uint32_t)T, &h);
+    Error e = Hasher::Create(ctxs, 256 << 10, 4u * (uint32_t)T + 64, (uint32_t)T, &h);
     if (e) {
       fprintf(stderr, "Hasher::Create: %s\n", e.msg.c_str());
       return 1;
@@ -146,10 +158,11 @@ int main(int argc, char** argv) {
     for (auto& x : th) x.join();
     secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     delete h;
-    printf("{\"workload\": \"receiver\", \"threads\": %d, \"uploads\": %ld, \"upload_bytes\": %zu, \"patch_bytes\": %zu, "
+    for (size_t g = 1; g < ctxs.size(); ++g) efes_ctx_destroy(ctxs[g]);
+    printf("{\"workload\": \"receiver\", \"gpus\": %d, \"threads\": %d, \"uploads\": %ld, \"upload_bytes\": %zu, \"patch_bytes\": %zu, "
            "\"read_bytes\": 32768, \"dir_fs\": \"%s\", \"seconds\": %.4f, \"value\": %.3f, \"unit\": \"GiB/s\", "
            "\"sum_sha1_crc32\": \"%s\", \"all_sums_equal\": %s, \"errors\": %d}\n",
-           T, T * U, S, P, fs_name(dir), secs, (double)T * U * S / secs / (1u << 30), first.c_str(),
+           G, T, T * U, S, P, fs_name(dir), secs, (double)T * U * S / secs / (1u << 30), first.c_str(),
            bad ? "false" : "true", errs.load());
   } else if (mode == "sha1file") {
     // One source file read by every thread U times through Sha1File (32 KiB reads).

@@ -18,13 +18,19 @@
 //
 // Search: longest-first order; cuts d1 <= d2 at length boundaries; part 0 = jobs [0, d1) in
 // shape g0 and part 1 = [d1, d2) in shape g1, each on CUs of its own (exclusive: its waves run
-// alone, at the lone-wave latency); the rest [d2, n) WIDE on the CUs left over, joined by the
-// exclusive parts' CUs as those finish.  The best such plan may then take a third exclusive part
-// [d2, d3) (e.g. the 16 MiB class of configs[3] as WIDE with one wave per SIMD, whose lanes
-// otherwise share SIMDs and set the tail).  Makespan = max(exclusive latencies, WIDE drain time,
-// longest WIDE job's latency); within 2 % the plan with less total issue work wins.  Measured on the
-// mixed config (configs[3]): WIDE waves sharing SIMDs with deep waves lose to them (older
-// waves issue first), which is why the deep parts get CUs of their own.
+// alone, at the lone-wave latency); the rest [d2, n) WIDE on the CUs left over, joined by each
+// CU of the exclusive parts as that CU's last workgroup ends.  An exclusive part gets
+// min(its workgroups, the CUs not yet taken) CUs and runs in rounds when it has more workgroups
+// than that: its workgroups are dealt longest-first to the earliest free CU (an LPT schedule,
+// as the dispatcher places them), so a part may hold several length classes -- on configs[3]
+// FED4E takes the 64 MiB class and GROUP4 the 32, 16 and 8 MiB classes in rounds on the other
+// 130 CUs, leaving the rest to WIDE once they free (0.887 s measured, against 0.99 s for GROUP4
+// on the 32 MiB class alone with a WIDE part that ends last).  The best such plan may then take
+// a third exclusive part [d2, d3).  Makespan = max(exclusive parts' ends, WIDE drain time,
+// the longest WIDE job's latency from when the WIDE part gets its first CU); within 0.5 % the
+// plan with less total issue work wins.  Measured on the mixed config (configs[3]): WIDE waves
+// sharing SIMDs with deep waves lose to them (older waves issue first), which is why the deep
+// parts get CUs of their own.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -33,6 +39,8 @@
 #include <algorithm>
 #include <cmath>
 #include <numeric>
+#include <tuple>
+#include <unordered_map>
 #include <utility>
 #include <vector>
 
@@ -116,15 +124,15 @@ int efes_plan_batch(efes_ctx* ctx, const uint64_t* lengths, uint32_t n, uint32_t
   auto blocks = [&](uint32_t i) { return i < n ? (double)(lengths[idx[i]] >> 6) : 0.0; };
   const double cus = ctx ? (double)ctx->cus : 256.0;
 
-  // cut candidates: where the length changes, thinned to <= 96 by cumulative blocks
+  // cut candidates: where the length changes, thinned to <= 64 by cumulative blocks
   std::vector<uint32_t> cuts{0};
   for (uint32_t i = 1; i < n; ++i)
     if (blocks(i) != blocks(i - 1)) cuts.push_back(i);
   cuts.push_back(n);
-  if (cuts.size() > 96) {
+  if (cuts.size() > 64) {
     std::vector<uint32_t> thin{0};
-    for (int q = 1; q < 95; ++q) {
-      const double target = pre[n] * q / 95.0;
+    for (int q = 1; q < 63; ++q) {
+      const double target = pre[n] * q / 63.0;
       const uint32_t i = (uint32_t)(std::lower_bound(pre.begin(), pre.end(), target) - pre.begin());
       auto it = std::lower_bound(cuts.begin(), cuts.end(), std::min(i, n));
       if (it != cuts.end() && *it != thin.back()) thin.push_back(*it);
@@ -135,68 +143,147 @@ int efes_plan_batch(efes_ctx* ctx, const uint64_t* lengths, uint32_t n, uint32_t
 
   // Every DEEP/GROUP part is exclusive (its workgroups own their CUs, so its waves run alone at
   // the lone-wave latency); WIDE runs on the CUs left over and on those the deep parts free.
-  // Part 1 may also be WIDE on CUs of its own (one wave per SIMD: its lanes at the lone-wave rate).
+  // A part may also be WIDE on CUs of its own (one wave per SIMD: its lanes at the lone-wave rate).
   const int shapes[] = {64, 32, 16, 8, 4, kFed, kFedE, kWideLanes};
-  auto deep_time = [&](int g, uint32_t first, uint32_t jobs, double* cus_out) {
-    const double c = std::ceil(waves(g, jobs) / 4.0);
-    *cus_out = std::min(c, cus);
-    const double lat = g == kWideLanes ? 740.0 * kCpiWideExclusive : latency(g);
-    return blocks(first) * lat * std::ceil(c / cus);  // rounds of workgroups beyond one per CU
+  // next[i]: the first job after i (longest-first) with fewer blocks than job i.
+  std::vector<uint32_t> next(n);
+  for (uint32_t i = n; i-- > 0;) next[i] = (i + 1 < n && blocks(i + 1) == blocks(i)) ? next[i + 1] : i + 1;
+  auto jobs_per_wg = [](int g) -> uint32_t {  // one workgroup per CU when exclusive
+    if (is_fed(g)) return (uint32_t)fed_jobs_per_cu(g);
+    if (g == kWideLanes) return 256u;  // four WIDE waves, one per SIMD
+    return 4u * (64u / (uint32_t)g);   // DEEP: 4 jobs; GROUPn: four waves of 64/n jobs
   };
-  // Makespan of a candidate: exclusive parts ps[0..k) (jobs [previous end, end) in shape g, on
-  // CUs of their own) concurrent with a WIDE part for the remaining jobs, which drains through
-  // the CUs left over and is joined by each exclusive part's CUs as that part ends.
+  struct Bucket {  // n CUs free from time t on
+    double t, n;
+  };
+  // An exclusive part [first, end) in shape g on c CUs: its workgroups (consecutive jobs,
+  // longest first, so a workgroup lasts as long as its first job's chain) are dealt to the
+  // earliest free CU, as the dispatcher does; returns the part's end and, in `out`, the times
+  // its CUs become free for the WIDE part.  Workgroups are dealt in bulk by runs of equal length
+  // (lengths within 12 % of a run's first count as the run's: the model errs long; at most ~55
+  // runs between 64 KiB and 64 MiB), so a part costs O(runs x distinct free times) whatever its
+  // job count.
+  auto lpt = [&](int g, uint32_t first, uint32_t end, double c, std::vector<Bucket>& out) -> double {
+    // `out` stays sorted by time; out[head..] are the CUs still to be dealt workgroups.
+    out.assign(1, Bucket{0.0, c});
+    size_t head = 0;
+    const uint32_t per = jobs_per_wg(g);
+    const double lat = g == kWideLanes ? 740.0 * kCpiWideExclusive : latency(g);
+    double tend = 0;
+    for (uint32_t w = first; w < end;) {
+      uint32_t run = std::min(next[w], end);  // jobs [w, run) within 12 % of w's length
+      while (run < end && blocks(run) >= 0.88 * blocks(w)) run = std::min(next[run], end);
+      const uint32_t wgs = (run - w + per - 1) / per;  // workgroups starting in the run
+      const double d = blocks(w) * lat;
+      double left = wgs;
+      while (left > 0) {
+        Bucket& e = out[head];  // the earliest free CUs
+        const double take = std::min(left, e.n), t1 = e.t + d;
+        e.n -= take;
+        if (e.n <= 0) ++head;
+        auto pos = std::lower_bound(out.begin() + (ptrdiff_t)head, out.end(), t1,
+                                    [](const Bucket& x, double t) { return x.t < t; });
+        if (pos != out.end() && pos->t == t1) pos->n += take;
+        else out.insert(pos, Bucket{t1, take});
+        tend = std::max(tend, t1);
+        left -= take;
+      }
+      w += wgs * per;
+    }
+    out.erase(out.begin(), out.begin() + (ptrdiff_t)head);
+    return tend;
+  };
+  struct Lpt {
+    double tend;
+    std::vector<Bucket> frees;
+  };
+  struct KeyHash {
+    size_t operator()(const std::tuple<int, uint32_t, uint32_t, int>& k) const {
+      return std::hash<uint64_t>()(((uint64_t)std::get<1>(k) * 0x9E3779B97F4A7C15ull) ^ ((uint64_t)std::get<2>(k) << 20) ^
+                                   ((uint64_t)std::get<0>(k) << 8) ^ (uint64_t)std::get<3>(k));
+    }
+  };
+  std::unordered_map<std::tuple<int, uint32_t, uint32_t, int>, Lpt, KeyHash> lpt_cache;
+  auto lpt_cached = [&](int g, uint32_t first, uint32_t end, double c) -> const Lpt& {
+    const auto key = std::make_tuple(g, first, end, (int)c);
+    auto it = lpt_cache.find(key);
+    if (it != lpt_cache.end()) return it->second;
+    Lpt r;
+    r.tend = lpt(g, first, end, c, r.frees);
+    return lpt_cache.emplace(key, std::move(r)).first->second;
+  };
+  // Makespan of a candidate: exclusive parts ps[0..k) (jobs [previous end, end) in shape g, each
+  // on min(its workgroups, CUs not yet taken) CUs, in rounds when it has more workgroups than
+  // that) concurrent with a WIDE part for the remaining jobs, which drains through the CUs left
+  // over and is joined by each CU of an exclusive part as that CU's last workgroup ends.
   struct Part {
     uint32_t end;
     int g;
   };
-  auto evaluate = [&](const Part* ps, int k, double* work_out) -> double {
-    double t = 0, wk = 0, used = 0;
-    std::pair<double, double> fin[EFES_PLAN_MAX_PARTS];  // (end time, CUs) of each exclusive part
-    int nf = 0;
-    uint32_t start = 0;
-    for (int i = 0; i < k; ++i) {
-      if (ps[i].end <= start) continue;
-      double c = 0;
-      const double ti = deep_time(ps[i].g, start, ps[i].end - start, &c);
-      t = std::max(t, ti);
-      wk += (pre[ps[i].end] - pre[start]) * work(ps[i].g, false);
-      used += c;
-      fin[nf++] = {ti, c};
-      start = ps[i].end;
-    }
-    *work_out = wk;
-    if (used > cus || (start < n && used >= cus)) return -1;  // does not fit
-    if (start < n) {
-      const double free0 = 4.0 * (cus - used);
-      const double w = waves(kWideLanes, n - start);
-      const double need = (pre[n] - pre[start]) * work(kWideLanes, w > 1.5 * free0);
-      *work_out += need;
-      std::sort(fin, fin + nf);
-      double done = 0, tw = -1, t_prev = 0, rate = free0;
-      for (int i = 0; i <= nf && tw < 0; ++i) {
-        const double t_end = i < nf ? fin[i].first : 1e300;
-        const double cap = (t_end - t_prev) * rate;
-        if (done + cap >= need) tw = t_prev + (need - done) / rate;
-        done += cap;
-        t_prev = t_end;
-        if (i < nf) rate += 4.0 * fin[i].second;
-      }
-      // the longest WIDE job runs alone on its SIMD only if every WIDE wave has one
-      const double stretch = w > free0 ? 2.0 / kWideShare : 1.0;
-      t = std::max(t, std::max(tw, blocks(start) * 740.0 * kCpiWideBusy * stretch));
-    }
-    return t;
-  };
-  // equal makespans (within 2 %): prefer less issue work (fewer busy SIMDs, higher clock)
   Part best[EFES_PLAN_MAX_PARTS - 1] = {};
   int best_k = 0;
   double best_t = -1, best_work = 0;
+  std::vector<Bucket> frees;
+  auto evaluate = [&](const Part* ps, int k, double* work_out) -> double {
+    double t = 0, wk = 0, used = 0;
+    frees.clear();
+    uint32_t start = 0;
+    for (int i = 0; i < k; ++i) {
+      if (ps[i].end <= start) continue;
+      const double need = std::ceil(waves(ps[i].g, ps[i].end - start) / 4.0);
+      const double c = std::min(need, cus - used);
+      if (c < 1) return -1;  // no CU left for this part
+      // a part's lower bound (its longest chain) already above the best plan: not worth an LPT
+      // ... nor its work spread over the CUs it gets
+      const double lat_i = ps[i].g == kWideLanes ? 740.0 * kCpiWideExclusive : latency(ps[i].g);
+      const double lb = std::max(blocks(start) * lat_i,
+                                 (pre[ps[i].end] - pre[start]) * lat_i / (double)jobs_per_wg(ps[i].g) / c);
+      if (best_t > 0 && lb > best_t * 1.005) return -1;
+      const Lpt& r = lpt_cached(ps[i].g, start, ps[i].end, c);
+      t = std::max(t, r.tend);
+      wk += (pre[ps[i].end] - pre[start]) * work(ps[i].g, false);
+      used += c;
+      const size_t mid = frees.size();  // both runs sorted by time: merge, not sort
+      frees.insert(frees.end(), r.frees.begin(), r.frees.end());
+      std::inplace_merge(frees.begin(), frees.begin() + (ptrdiff_t)mid, frees.end(),
+                         [](const Bucket& x, const Bucket& y) { return x.t < y.t; });
+      start = ps[i].end;
+    }
+    *work_out = wk;
+    if (start < n) {
+      const double free0 = 4.0 * (cus - used);  // SIMDs
+      if (free0 <= 0 && frees.empty()) return -1;
+      const double w = waves(kWideLanes, n - start);
+      const double need = (pre[n] - pre[start]) * work(kWideLanes, w > 1.5 * std::max(free0, 4.0));
+      *work_out += need;
+      double done = 0, tw = -1, t_prev = 0, rate = free0;
+      double t_first = free0 > 0 ? 0.0 : -1, simds_first = free0;  // when the WIDE part starts
+      for (size_t i = 0; i <= frees.size() && tw < 0; ++i) {
+        const double t_end = i < frees.size() ? frees[i].t : 1e300;
+        const double cap = (t_end - t_prev) * rate;
+        if (rate > 0 && done + cap >= need) tw = t_prev + (need - done) / rate;
+        done += cap;
+        t_prev = t_end;
+        if (i < frees.size()) {
+          rate += 4.0 * frees[i].n;
+          if (t_first < 0) {
+            t_first = frees[i].t;
+            simds_first = 4.0 * frees[i].n;
+          }
+        }
+      }
+      // the longest WIDE job runs alone on its SIMD only if every WIDE wave has one
+      const double stretch = w > simds_first ? 2.0 / kWideShare : 1.0;
+      t = std::max(t, std::max(tw, t_first + blocks(start) * 740.0 * kCpiWideBusy * stretch));
+    }
+    return t;
+  };
+  // equal makespans (within 0.5 %): prefer less issue work (fewer busy SIMDs, higher clock)
   auto consider = [&](const Part* ps, int k) {
     double wk = 0;
     const double t = evaluate(ps, k, &wk);
     if (t < 0) return;
-    if (best_t < 0 || t < best_t * 0.98 || (t < best_t * 1.02 && wk < best_work)) {
+    if (best_t < 0 || t < best_t * 0.995 || (t < best_t * 1.005 && wk < best_work)) {
       std::copy(ps, ps + k, best);
       best_k = k;
       best_t = t;

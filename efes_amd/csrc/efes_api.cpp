@@ -224,13 +224,15 @@ int efes_auto_mode(const efes_ctx* ctx, uint32_t njobs) {
   // The lowest per-job latency that fits in one pass: DEEP up to one job per
   // SIMD (46.5 ms per 4 MiB job); FED4 up to 32 jobs per CU (48.5 ms: DEEP's chain, fed from
   // two producer SIMDs -- below GROUP32/16/8's 49/52/57 ms at 2/4/8 jobs per SIMD); FED4E up to
-  // 48 per CU (55.5 ms); grouped DEEP G = 4 (67 ms, 64 jobs per CU) up to 24 jobs per SIMD; WIDE
-  // beyond, once its lanes (~40 MB/s each) outrun GROUP4 (which saturates at one wave per SIMD).
+  // 48 per CU (55.5 ms); grouped DEEP G = 4 (67 ms, 64 jobs per CU) up to 16 jobs per SIMD, i.e.
+  // one GROUP4 wave per SIMD; WIDE beyond: a second GROUP4 wave on a SIMD doubles the launch
+  // (134 ms), while WIDE lanes (~40 MB/s each) take 108 ms for any count up to a wave per SIMD
+  // (measured 18 432-24 576 x 4 MiB: WIDE 668-883 GiB/s, GROUP4 534-715, tools/gpu_auto_band.sh).
   const uint64_t simds = 4ull * (ctx ? (uint64_t)ctx->cus : 256ull), n = njobs;
   if (n <= simds) return EFES_MODE_DEEP;
   if (n <= 8 * simds) return EFES_MODE_FED4;
   if (n <= 12 * simds) return EFES_MODE_FED4E;  // 55.5 ms, 48 jobs per CU
-  if (n <= 24 * simds) return EFES_MODE_GROUP4;
+  if (n <= 16 * simds) return EFES_MODE_GROUP4;
   return EFES_MODE_WIDE;
 }
 

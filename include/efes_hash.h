@@ -135,7 +135,7 @@ int efes_hash_submit(efes_ctx* ctx, const efes_job* jobs_device, uint32_t njobs,
 int efes_hash_submit_mode(efes_ctx* ctx, const efes_job* jobs_device, uint32_t njobs, void* stream, int mode);
 /* The shape EFES_MODE_AUTO picks for njobs jobs of similar length (ctx may be NULL: one
  * MI355X): DEEP up to one job per SIMD, FED4 up to 32 per CU, FED4E up to 48 per CU, GROUP4 up to
- * 24 per SIMD, WIDE beyond. */
+ * 16 per SIMD (one wave each), WIDE beyond. */
 int efes_auto_mode(const efes_ctx* ctx, uint32_t njobs);
 /* Mixed-length batches (BASELINE configs[3], concurrent uploads of different sizes): the
  * makespan is set by the longest jobs (a SHA-1 chain per job), so a batch is cut, longest

@@ -175,7 +175,7 @@ def test_auto_mode_by_job_count(efes_lib):
     G = efes_lib.MODE_GROUP
     F, FE = efes_lib.MODE_FED4, efes_lib.MODE_FED4E
     want = {1: efes_lib.MODE_DEEP, 1024: efes_lib.MODE_DEEP, 1025: F, 2048: F, 4096: F, 8192: F, 8193: FE,
-            12288: FE, 12289: G[4], 24576: G[4], 24577: efes_lib.MODE_WIDE, 131072: efes_lib.MODE_WIDE}
+            12288: FE, 12289: G[4], 16384: G[4], 16385: efes_lib.MODE_WIDE, 131072: efes_lib.MODE_WIDE}
     assert {n: L.efes_auto_mode(None, n) for n in want} == want
 
 

@@ -113,6 +113,8 @@ SIGNATURES = {
     "efes_queue_destroy": (None, [_VP]),
     "efes_upload_open": (_I, [_VP, _U32, _P(Sha1State), _P(Crc32State), _P(_VP)]),
     "efes_upload_write": (_I, [_VP, _VP, _S]),
+    "efes_upload_reserve": (_I, [_VP, _S, _P(_VP), _P(_S)]),
+    "efes_upload_commit": (_I, [_VP, _S]),
     "efes_upload_flush": (_I, [_VP]),
     "efes_upload_state": (_I, [_VP, _P(Sha1State), _P(Crc32State)]),
     "efes_upload_sum": (_I, [_VP, _VP]),

@@ -316,11 +316,13 @@ int efes_upload_write(efes_upload* u, const void* p, size_t n) {
     // Go compresses a full pending tail even on an empty Write (sha1.go:61-69); run a
     // zero-length job so the device state follows.
     std::unique_lock<std::mutex> lk(q->mu);
-    enqueue_current(u, lk);
-    q->freed.wait(lk, [&] { return !q->free_chunks.empty() || q->fault; });
-    if (q->fault) return u->latched = q->fault;
-    u->cur = (int32_t)q->free_chunks.back();
-    q->free_chunks.pop_back();
+    enqueue_current(u, lk);  // hands a partly filled chunk over; an empty reserved one stays
+    if (u->cur < 0) {
+      q->freed.wait(lk, [&] { return !q->free_chunks.empty() || q->fault; });
+      if (q->fault) return u->latched = q->fault;
+      u->cur = (int32_t)q->free_chunks.back();
+      q->free_chunks.pop_back();
+    }
     u->fill = 0;
     enqueue_current(u, lk, true);
     return EFES_OK;
@@ -346,6 +348,45 @@ int efes_upload_write(efes_upload* u, const void* p, size_t n) {
       std::unique_lock<std::mutex> lk(q->mu);
       enqueue_current(u, lk);
     }
+  }
+  return EFES_OK;
+}
+
+int efes_upload_reserve(efes_upload* u, size_t min_bytes, void** p, size_t* n) {
+  if (!u || !p || !n) return EFES_ERR_ARG;
+  if (u->latched) return u->latched;
+  efes_queue* q = u->q;
+  const uint64_t want = std::max<uint64_t>(1, std::min<uint64_t>(min_bytes, q->chunk));
+  if (u->cur >= 0 && q->chunk - u->fill < want) {  // too little room left: hand the chunk over
+    std::unique_lock<std::mutex> lk(q->mu);
+    enqueue_current(u, lk);
+  }
+  if (u->cur < 0) {
+    std::unique_lock<std::mutex> lk(q->mu);
+    q->freed.wait(lk, [&] { return !q->free_chunks.empty() || q->fault; });  // back-pressure
+    if (q->fault) return u->latched = q->fault;
+    u->cur = (int32_t)q->free_chunks.back();
+    q->free_chunks.pop_back();
+    u->fill = 0;
+  }
+  *p = q->h_slab + (size_t)u->cur * q->chunk + u->fill;
+  *n = (size_t)(q->chunk - u->fill);
+  return EFES_OK;
+}
+
+int efes_upload_commit(efes_upload* u, size_t k) {
+  if (!u) return EFES_ERR_ARG;
+  if (u->latched) return u->latched;
+  if (k == 0) return efes_upload_write(u, nullptr, 0);  // Write(empty): sha1.go:61-69 still runs
+  efes_queue* q = u->q;
+  if (u->cur < 0 || k > q->chunk - u->fill) return EFES_ERR_ARG;  // not within the reserved room
+  const uint8_t* src = q->h_slab + (size_t)u->cur * q->chunk + u->fill;
+  const int rc = efes::replay_write(&u->shadow, src, k);
+  if (rc) return u->latched = rc;  // the Go Write would panic (nx > 64)
+  u->fill += k;
+  if (u->fill == q->chunk) {
+    std::unique_lock<std::mutex> lk(q->mu);
+    enqueue_current(u, lk);
   }
   return EFES_OK;
 }

@@ -701,21 +701,28 @@ Error saveFile(Hasher* h, const std::string& path, int64_t offset, int64_t lengt
   if (rc) return lib_error(rc);
 
   // n, _ := io.Copy(w, r) (filereceiver.go:209): 32 KiB buffers; a read error ends the copy
-  // and is ignored, so the bytes read so far still advance the state.
-  std::vector<uint8_t> buf(32 << 10);
+  // and is ignored, so the bytes read so far still advance the state.  The buffer IS the
+  // upload's pinned staging (efes_upload_reserve): the body is read straight into it, the file
+  // written from it, and the commit hashes it in place -- one host copy fewer than a Write.
+  constexpr size_t kCopyBuf = 32 << 10;
   int64_t n = 0;
   for (;;) {
+    void* sp = nullptr;
+    size_t room = 0;
+    rc = efes_upload_reserve(g.u, kCopyBuf, &sp, &room);
+    if (rc) return lib_error(rc);  // the .info keeps its old offset
+    uint8_t* buf = static_cast<uint8_t*>(sp);
     Error er;
-    const size_t nr = r.Read(buf.data(), buf.size(), &er);
+    const size_t nr = r.Read(buf, std::min(room, kCopyBuf), &er);
     if (nr > 0) {
       size_t nw = 0;
-      Error ew = write_full(f.fd, path, buf.data(), nr, &nw);
+      Error ew = write_full(f.fd, path, buf, nr, &nw);
       if (ew) {  // MultiWriter stops at the file: the digests never see this buffer
         n += (int64_t)nw;
         break;
       }
-      rc = efes_upload_write(g.u, buf.data(), nr);  // CRC32.Write, Sha1.Write
-      if (rc) return lib_error(rc);                   // the .info keeps its old offset
+      rc = efes_upload_commit(g.u, nr);  // CRC32.Write, Sha1.Write
+      if (rc) return lib_error(rc);
       n += (int64_t)nr;
     }
     if (er) break;

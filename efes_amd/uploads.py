@@ -69,6 +69,17 @@ class Upload:
         check(lib().efes_upload_write(self._h, ptr, n), "Upload.write")
         return n
 
+    def reserve(self, min_bytes: int) -> memoryview:
+        """efes_upload_reserve: a writable view of >= min(min_bytes, chunk) bytes of the upload's
+        pinned staging chunk (zero-copy: fill it, then commit(k))."""
+        p, n = ctypes.c_void_p(), ctypes.c_size_t()
+        check(lib().efes_upload_reserve(self._h, min_bytes, ctypes.byref(p), ctypes.byref(n)), "Upload.reserve")
+        return memoryview((ctypes.c_uint8 * n.value).from_address(p.value)).cast("B")
+
+    def commit(self, k: int) -> None:
+        """efes_upload_commit: the first k reserved bytes are one Write(p[:k]) (sha1.go:58-79)."""
+        check(lib().efes_upload_commit(self._h, k), "Upload.commit")
+
     def flush(self) -> None:
         check(lib().efes_upload_flush(self._h), "Upload.flush")
 

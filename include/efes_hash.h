@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define EFES_ABI_VERSION 2
+#define EFES_ABI_VERSION 3
 
 /* ---- error codes ---------------------------------------------------------------- */
 #define EFES_OK 0
@@ -228,6 +228,14 @@ void efes_queue_destroy(efes_queue* q); /* finishes launched work; close uploads
 int efes_upload_open(efes_queue* q, uint32_t hashes, const efes_sha1_state* sha1, const efes_crc32_state* crc32,
                      efes_upload** out);
 int efes_upload_write(efes_upload* u, const void* p, size_t n);
+/* Zero-copy staging (ABI 3): *p / *n = at least min(min_bytes, chunk_bytes) contiguous bytes of
+ * the upload's pinned staging chunk (a partly filled chunk with less room is handed to the
+ * dispatcher first; blocks while every chunk is in use).  Fill k <= *n of them -- read a request
+ * body straight in, write the file from there -- and efes_upload_commit(u, k): the same as
+ * efes_upload_write of those k bytes (one Write of k bytes, sha1.go:58-79) without the copy.
+ * Bytes reserved but not committed are dropped; reserve again before the next commit. */
+int efes_upload_reserve(efes_upload* u, size_t min_bytes, void** p, size_t* n);
+int efes_upload_commit(efes_upload* u, size_t k);
 int efes_upload_flush(efes_upload* u);
 int efes_upload_state(efes_upload* u, efes_sha1_state* sha1, efes_crc32_state* crc32);
 int efes_upload_sum(efes_upload* u, uint8_t out[24]);

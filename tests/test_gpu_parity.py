@@ -612,6 +612,56 @@ def test_upload_midstream_state_then_continue(env, oracle):
         up2.close()
 
 
+def test_upload_reserve_commit_equals_write(env, oracle):
+    """Zero-copy staging (efes_upload_reserve / commit, ABI 3): the same Write sequence through
+    reserve + fill + commit and through efes_upload_write gives the same state, MarshalText and
+    Sums; a reservation larger than the chunk's room hands the chunk over early; commit(0) is
+    Go's empty Write (a pending full tail is compressed); a commit beyond the room is refused."""
+    from efes_amd._lib import Sha1State
+    from efes_amd.uploads import UploadQueue
+    efes = env["efes"]
+    rng = random.Random(5)
+    data = oracle.fill_synthetic(3 << 20, 77).tobytes()
+    with UploadQueue(env["ctx"], chunk_bytes=64 * 1024, max_chunks=16, max_uploads=4) as q:
+        for trial in range(6):
+            a, b = q.open(), q.open()
+            o = oracle.Sha1()
+            pos = 0
+            while pos < len(data) // (trial + 1):
+                n = min(rng.choice([0, 1, 63, 64, 65, 4096, 32 * 1024, 40000, 64 * 1024]), len(data) - pos)
+                want = rng.choice([1, n or 1, 32 * 1024, 64 * 1024, 1 << 20])
+                a.write(data[pos:pos + n])
+                view = b.reserve(want)
+                assert len(view) >= min(max(want, 1), 64 * 1024)
+                if n > len(view):  # reserve what the piece needs, as saveFile does
+                    view = b.reserve(n)
+                view[:n] = data[pos:pos + n]
+                b.commit(n)
+                o.write(data[pos:pos + n])
+                pos += n
+            assert a.marshal_text() == b.marshal_text()
+            assert b.marshal_text()[0].decode() == o.marshal_text()
+            assert a.sums() == b.sums() == (hashlib.sha1(data[:pos]).digest(), zlib.crc32(data[:pos]))
+            a.close()
+            b.close()
+        # commit(0) on a pending full tail (nx == 64, only reachable through UnmarshalText)
+        o = oracle.Sha1()
+        o.write(data[:64])
+        st = Sha1State()
+        st.h[:] = [0x67452301, 0xEFCDAB89, 0x98BADCFE, 0x10325476, 0xC3D2E1F0]
+        st.x[:] = data[:64]
+        st.nx, st.len = 64, 64
+        up = q.open(st)
+        up.reserve(1)
+        up.commit(0)
+        assert up.sums()[0] == hashlib.sha1(data[:64]).digest()
+        view = up.reserve(16)
+        with pytest.raises(efes.EfesError) as e:
+            up.commit(len(view) + 1)
+        assert e.value.code == efes.EFES_ERR_ARG
+        up.close()
+
+
 def test_upload_queue_limits(env):
     from efes_amd.uploads import UploadQueue
     efes = env["efes"]

@@ -9,6 +9,8 @@
 //                                 (gpus > 1: one process over several GPUs, a queue per GPU, each
 //                                  PATCH on the least-loaded one -- a storage server is one process)
 //   tools/bench_receiver sha1file <dir> <threads> <files_per_thread> <file_bytes>
+//   tools/bench_receiver files    <dir> <threads> <files_per_thread> <file_bytes>   (no hashing:
+//                                 the file-system side of the receiver alone)
 //
 // Every upload carries the same bytes, so every finished upload must report the digests of a
 // reference upload made before the clock starts; each file is removed when its upload is done
@@ -89,7 +91,7 @@ Response upload(FileReceiver& fr, const std::string& path, const std::vector<uin
 }  // namespace
 
 int main(int argc, char** argv) {
-  if (argc < 7 && !(argc >= 6 && std::string(argv[1]) == "sha1file")) {
+  if (argc < 7 && !(argc >= 6 && (std::string(argv[1]) == "sha1file" || std::string(argv[1]) == "files"))) {
     fprintf(stderr,
             "usage: %s receiver <dir> <threads> <uploads_per_thread> <upload_bytes> <patch_bytes>\n"
             "       %s sha1file <dir> <threads> <files_per_thread> <file_bytes>\n",
@@ -164,6 +166,37 @@ int main(int argc, char** argv) {
            "\"sum_sha1_crc32\": \"%s\", \"all_sums_equal\": %s, \"errors\": %d}\n",
            G, T, T * U, S, P, fs_name(dir), secs, (double)T * U * S / secs / (1u << 30), first.c_str(),
            bad ? "false" : "true", errs.load());
+  } else if (mode == "files") {
+    // The file-system side of the receiver alone (no hashing): per upload, create + 32 KiB
+    // writes + fsync + close + unlink, T threads -- the ceiling the receiver can reach here.
+    auto t0 = std::chrono::steady_clock::now();
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t)
+      th.emplace_back([&, t] {
+        const std::string d = dir + "/files/" + std::to_string(t);
+        if (system(("mkdir -p '" + d + "'").c_str()) != 0) {
+          ++errs;
+          return;
+        }
+        for (long u = 0; u < U; ++u) {
+          const std::string path = d + "/" + std::to_string(u) + ".fid";
+          FILE* f = fopen(path.c_str(), "wb");
+          if (!f) {
+            ++errs;
+            return;
+          }
+          for (size_t a = 0; a < S; a += 32 << 10)
+            if (fwrite(src.data() + a, 1, std::min<size_t>(32 << 10, S - a), f) == 0) ++errs;
+          fflush(f);
+          if (fsync(fileno(f)) != 0 || fclose(f) != 0) ++errs;
+          unlink(path.c_str());
+        }
+      });
+    for (auto& x : th) x.join();
+    secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    printf("{\"workload\": \"files\", \"threads\": %d, \"files\": %ld, \"file_bytes\": %zu, \"dir_fs\": \"%s\", "
+           "\"seconds\": %.4f, \"value\": %.3f, \"unit\": \"GiB/s\", \"errors\": %d}\n",
+           T, T * U, S, fs_name(dir), secs, (double)T * U * S / secs / (1u << 30), errs.load());
   } else if (mode == "sha1file") {
     // One source file read by every thread U times through Sha1File (32 KiB reads).
     const std::string path = dir + "/bench_sha1file.dat";

@@ -226,13 +226,9 @@ __device__ void deep_bulk(const Tables& T, int lane, const uint8_t* q, uint64_t 
     if (do_sha) {
       uint32_t hv[5] = {h[0], h[1], h[2], h[3], h[4]}, hs[5];
       auto block = [&]() {
-        uint32_t s[5] = {hv[0], hv[1], hv[2], hv[3], hv[4]};
-        ChainRegs<0>::run(s, x);
+        chain_block(hv, x, hs);  // sha1.go:193-197 folded in
 #pragma unroll
-        for (int k = 0; k < 5; ++k) {
-          hs[k] = hv[k] + s[k];                                                       // sha1.go:193-197
-          hv[k] = (uint32_t)__builtin_amdgcn_mov_dpp((int)hs[k], 0x138, 0xf, 0xf, true);  // wave_shr:1
-        }
+        for (int k = 1; k < 6; ++k) hv[k % 5] = (uint32_t)__builtin_amdgcn_mov_dpp((int)hs[k % 5], 0x138, 0xf, 0xf, true);  // wave_shr:1, h0 (round 79's v_add3) last
       };
       const int nbu = (int)uniform32((uint32_t)nb);
       int j = 0;
@@ -553,13 +549,9 @@ __device__ void pipe_consume(PipeSlot& P, int lane, uint64_t nbulk, uint32_t (&h
     lds_release(&P.taken, step + 1);  // (release: the reads above complete first)
     uint32_t hv[5] = {h[0], h[1], h[2], h[3], h[4]}, hs[5];
     auto block = [&]() {
-      uint32_t s[5] = {hv[0], hv[1], hv[2], hv[3], hv[4]};
-      ChainRegs<0>::run(s, x);
+      chain_block(hv, x, hs);  // sha1.go:193-197 folded in
 #pragma unroll
-      for (int k = 0; k < 5; ++k) {
-        hs[k] = hv[k] + s[k];                                                           // sha1.go:193-197
-        hv[k] = (uint32_t)__builtin_amdgcn_mov_dpp((int)hs[k], 0x138, 0xf, 0xf, true);  // wave_shr:1
-      }
+      for (int k = 1; k < 6; ++k) hv[k % 5] = (uint32_t)__builtin_amdgcn_mov_dpp((int)hs[k % 5], 0x138, 0xf, 0xf, true);  // wave_shr:1, h0 (round 79's v_add3) last
     };
     const int nbu = (int)uniform32((uint32_t)nb);
     int j = 0;
@@ -685,13 +677,9 @@ __device__ void group_bulk(const Tables& T, const PosTables& P, int lane, DeepMs
     }
     if constexpr (kSha) {
       auto block = [&]() {
-        uint32_t s[5] = {hv[0], hv[1], hv[2], hv[3], hv[4]};
-        ChainRegs<0>::run(s, x);  // real in lane m*G+j of every job m at iteration j
+        chain_block(hv, x, hs);  // real in lane m*G+j of every job m at iteration j
 #pragma unroll
-        for (int k = 0; k < 5; ++k) {
-          hs[k] = hv[k] + s[k];
-          hv[k] = (uint32_t)__builtin_amdgcn_mov_dpp((int)hs[k], 0x138, 0xf, 0xf, true);  // wave_shr:1
-        }
+        for (int k = 1; k < 6; ++k) hv[k % 5] = (uint32_t)__builtin_amdgcn_mov_dpp((int)hs[k % 5], 0x138, 0xf, 0xf, true);  // wave_shr:1, h0 (round 79's v_add3) last
       };
 #pragma unroll
       for (int j = 0; j < G; j += 2) { block(); block(); }
@@ -1038,13 +1026,9 @@ __device__ void fed_consume(FedSlot& P, int lane, const DeepMsg* msgs, uint64_t 
     }
     ++gstep;
     auto block = [&]() {
-      uint32_t s[5] = {hv[0], hv[1], hv[2], hv[3], hv[4]};
-      ChainRegs<0>::run(s, x);  // real in lane m*G+j of every job m at iteration j
+      chain_block(hv, x, hs);  // real in lane m*G+j of every job m at iteration j
 #pragma unroll
-      for (int k = 0; k < 5; ++k) {
-        hs[k] = hv[k] + s[k];
-        hv[k] = (uint32_t)__builtin_amdgcn_mov_dpp((int)hs[k], 0x138, 0xf, 0xf, true);  // wave_shr:1
-      }
+      for (int k = 1; k < 6; ++k) hv[k % 5] = (uint32_t)__builtin_amdgcn_mov_dpp((int)hs[k % 5], 0x138, 0xf, 0xf, true);  // wave_shr:1, h0 (round 79's v_add3) last
     };
 #pragma unroll
     for (int j = 0; j < G; ++j) block();

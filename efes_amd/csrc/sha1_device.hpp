@@ -74,18 +74,33 @@ struct ChainQuad<20> {
   __device__ __forceinline__ static void run(uint32_t (&)[5], const uint4* __restrict__) {}
 };
 
-// ---- chain from W[i]+K[i] held in this lane's own registers (80 VGPRs).
-template <int R>
+// ---- chain from W[i]+K[i] held in this lane's own registers (80 VGPRs): rounds R..End-1.
+template <int R, int End = 80>
 struct ChainRegs {
   __device__ __forceinline__ static void run(uint32_t (&s)[5], const uint32_t (&wk)[80]) {
     round_wk<R>(s, wk[R]);
-    ChainRegs<R + 1>::run(s, wk);
+    ChainRegs<R + 1, End>::run(s, wk);
   }
 };
-template <>
-struct ChainRegs<80> {
+template <int End>
+struct ChainRegs<End, End> {
   __device__ __forceinline__ static void run(uint32_t (&)[5], const uint32_t (&)[80]) {}
 };
+
+// hs = hv + compress(hv, WK) (sha1.go:141-197) from W+K registers.  Round 79 writes a80 into
+// s[0], and a80 + h0 is the new h0, so h0 is folded into that round's e + W + K (one v_add3 in
+// place of a v_add there and the h0 add after it): 404 VALU per block instead of 405.
+__device__ __forceinline__ void chain_block(const uint32_t (&hv)[5], const uint32_t (&wk)[80], uint32_t (&hs)[5]) {
+  uint32_t s[5] = {hv[0], hv[1], hv[2], hv[3], hv[4]};
+  ChainRegs<0, 79>::run(s, wk);
+  // round 79 (R % 5 == 4): a, b, c, d, e = s[1], s[2], s[3], s[4], s[0]
+  const uint32_t z = add3(s[0], wk[79], hv[0]);
+  hs[0] = add3(rotl(s[1], 5), __builtin_amdgcn_bitop3_b32(s[2], s[3], s[4], round_lut<79>()), z);
+  hs[1] = hv[1] + s[1];
+  hs[2] = hv[2] + rotl(s[2], 30);
+  hs[3] = hv[3] + s[3];
+  hs[4] = hv[4] + s[4];
+}
 
 // h += compress(WK) -- sha1.go:141-197 with the schedule already expanded.
 __device__ __forceinline__ void compress_wk(uint32_t (&h)[5], const uint4* __restrict__ wk4) {

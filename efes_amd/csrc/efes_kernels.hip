@@ -611,6 +611,16 @@ __global__ __launch_bounds__(128 * kPipeJobs, 1) void deep_kernel(const efes_job
   }
 }
 
+// The value of the last lane of each group of G lanes, in every lane of the group: a job's
+// chaining value after a super-step, back to all its lanes.  G = 4 is one quad: a DPP
+// quad_perm [3,3,3,3] move (no LDS round trip on the chain's critical path); wider groups use
+// ds_bpermute.
+template <int G>
+__device__ __forceinline__ uint32_t group_last(uint32_t v, int lane) {
+  if constexpr (G == 4) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xFF, 0xf, 0xf, true);
+  return (uint32_t)__shfl((int)v, lane | (G - 1));
+}
+
 // ================================================================== grouped DEEP kernel
 // k = 64/G jobs per wave, G lanes (= G consecutive blocks per super-step) per job.  For
 // batches with more long jobs than SIMDs: the chain instructions are shared by the k jobs
@@ -685,7 +695,7 @@ __device__ void group_bulk(const Tables& T, const PosTables& P, int lane, DeepMs
       for (int j = 0; j < G; j += 2) { block(); block(); }
       // the job's chaining value is in its last lane: back to all G lanes (its first one needs it)
 #pragma unroll
-      for (int k = 0; k < 5; ++k) hv[k] = (uint32_t)__shfl((int)hs[k], lane | (G - 1));
+      for (int k = 0; k < 5; ++k) hv[k] = group_last<G>(hs[k], lane);
     }
   };
   uint32_t A[16], B[16];
@@ -1033,7 +1043,7 @@ __device__ void fed_consume(FedSlot& P, int lane, const DeepMsg* msgs, uint64_t 
 #pragma unroll
     for (int j = 0; j < G; ++j) block();
 #pragma unroll
-    for (int k = 0; k < 5; ++k) hv[k] = (uint32_t)__shfl((int)hs[k], lane | (G - 1));
+    for (int k = 0; k < 5; ++k) hv[k] = group_last<G>(hs[k], lane);
   }
   FED_STAT(stats[1] += __builtin_amdgcn_s_memtime() - t_begin; stats[2] += S;)
 }

@@ -29,6 +29,7 @@
 #include <vector>
 
 #include "../efes_amd/host/efes_receiver.hpp"
+#include "cpu_quota.hpp"
 
 using namespace efes;
 
@@ -91,6 +92,7 @@ Response upload(FileReceiver& fr, const std::string& path, const std::vector<uin
 }  // namespace
 
 int main(int argc, char** argv) {
+  const int pinned_cpus = pin_to_cpu_quota();  // see cpu_quota.hpp
   if (argc < 7 && !(argc >= 6 && (std::string(argv[1]) == "sha1file" || std::string(argv[1]) == "files"))) {
     fprintf(stderr,
             "usage: %s receiver <dir> <threads> <uploads_per_thread> <upload_bytes> <patch_bytes>\n"
@@ -161,10 +163,10 @@ int main(int argc, char** argv) {
     secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     delete h;
     for (size_t g = 1; g < ctxs.size(); ++g) efes_ctx_destroy(ctxs[g]);
-    printf("{\"workload\": \"receiver\", \"gpus\": %d, \"threads\": %d, \"uploads\": %ld, \"upload_bytes\": %zu, \"patch_bytes\": %zu, "
+    printf("{\"workload\": \"receiver\", \"pinned_cpus\": %d, \"gpus\": %d, \"threads\": %d, \"uploads\": %ld, \"upload_bytes\": %zu, \"patch_bytes\": %zu, "
            "\"read_bytes\": 32768, \"dir_fs\": \"%s\", \"seconds\": %.4f, \"value\": %.3f, \"unit\": \"GiB/s\", "
            "\"sum_sha1_crc32\": \"%s\", \"all_sums_equal\": %s, \"errors\": %d}\n",
-           G, T, T * U, S, P, fs_name(dir), secs, (double)T * U * S / secs / (1u << 30), first.c_str(),
+           pinned_cpus, G, T, T * U, S, P, fs_name(dir), secs, (double)T * U * S / secs / (1u << 30), first.c_str(),
            bad ? "false" : "true", errs.load());
   } else if (mode == "files") {
     // The file-system side of the receiver alone (no hashing): per upload, create + 32 KiB
@@ -194,9 +196,9 @@ int main(int argc, char** argv) {
       });
     for (auto& x : th) x.join();
     secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    printf("{\"workload\": \"files\", \"threads\": %d, \"files\": %ld, \"file_bytes\": %zu, \"dir_fs\": \"%s\", "
+    printf("{\"workload\": \"files\", \"pinned_cpus\": %d, \"threads\": %d, \"files\": %ld, \"file_bytes\": %zu, \"dir_fs\": \"%s\", "
            "\"seconds\": %.4f, \"value\": %.3f, \"unit\": \"GiB/s\", \"errors\": %d}\n",
-           T, T * U, S, fs_name(dir), secs, (double)T * U * S / secs / (1u << 30), errs.load());
+           pinned_cpus, T, T * U, S, fs_name(dir), secs, (double)T * U * S / secs / (1u << 30), errs.load());
   } else if (mode == "sha1file") {
     // One source file read by every thread U times through Sha1File (32 KiB reads).
     const std::string path = dir + "/bench_sha1file.dat";
@@ -241,10 +243,10 @@ int main(int argc, char** argv) {
     for (auto& x : th) x.join();
     secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     unlink(path.c_str());
-    printf("{\"workload\": \"sha1file\", \"threads\": %d, \"files\": %ld, \"file_bytes\": %zu, \"read_bytes\": 32768, "
+    printf("{\"workload\": \"sha1file\", \"pinned_cpus\": %d, \"threads\": %d, \"files\": %ld, \"file_bytes\": %zu, \"read_bytes\": 32768, "
            "\"dir_fs\": \"%s\", \"seconds\": %.4f, \"value\": %.3f, \"unit\": \"GiB/s\", \"sum_sha1\": \"%s\", "
            "\"all_sums_equal\": %s, \"errors\": %d}\n",
-           T, T * U, S, fs_name(dir), secs, (double)T * U * S / secs / (1u << 30), first.c_str(), bad ? "false" : "true",
+           pinned_cpus, T, T * U, S, fs_name(dir), secs, (double)T * U * S / secs / (1u << 30), first.c_str(), bad ? "false" : "true",
            errs.load());
   } else {
     fprintf(stderr, "unknown mode %s\n", mode.c_str());

@@ -17,8 +17,10 @@
 #include <vector>
 
 #include "efes_hash.h"
+#include "cpu_quota.hpp"
 
 int main(int argc, char** argv) {
+  const int pinned_cpus = pin_to_cpu_quota();  // see cpu_quota.hpp
   if (argc < 5) {
     fprintf(stderr, "usage: %s threads uploads upload_bytes write_bytes [open_per_thread] [chunk_bytes] [stagger]\n", argv[0]);
     return 2;
@@ -113,10 +115,10 @@ int main(int argc, char** argv) {
   efes_ctx_destroy(ctx);
   char hex[49];
   for (int i = 0; i < 24; ++i) snprintf(hex + 2 * i, 3, "%02x", first[i]);
-  printf("{\"workload\": \"uploads\", \"threads\": %d, \"uploads\": %ld, \"upload_bytes\": %zu, \"write_bytes\": %zu, "
+  printf("{\"workload\": \"uploads\", \"pinned_cpus\": %d, \"threads\": %d, \"uploads\": %ld, \"upload_bytes\": %zu, \"write_bytes\": %zu, "
          "\"open_per_thread\": %d, \"stagger\": %d, \"chunk_bytes\": %llu, \"max_chunks\": %u, \"seconds\": %.4f, \"value\": %.3f, \"unit\": \"GiB/s\", "
          "\"sum_sha1_crc32\": \"%s\", \"all_sums_equal\": %s, \"errors\": %d}\n",
-         T, U, S, W, K, stagger, (unsigned long long)chunk, max_chunks, secs, (double)U * S / secs / (1u << 30), hex,
+         pinned_cpus, T, U, S, W, K, stagger, (unsigned long long)chunk, max_chunks, secs, (double)U * S / secs / (1u << 30), hex,
          bad ? "false" : "true", errs.load());
   return errs || bad ? 1 : 0;
 }

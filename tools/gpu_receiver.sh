@@ -22,4 +22,6 @@ run sf_t1_16m      sha1file "$D" 1   2 $((16 << 20))
 run sf_t64_16m     sha1file "$D" 64  2 $((16 << 20))
 run sf_t256_16m    sha1file "$D" 256 2 $((16 << 20))
 run sf_t1024_4m    sha1file "$D" 1024 2 $M
+run files_t256     files "$D" 256 2 $M
+run files_t1024    files "$D" 1024 2 $M
 echo ALL_DONE

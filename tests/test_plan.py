@@ -103,3 +103,50 @@ def test_batch_larger_than_max_jobs_is_rejected():
     plan = Plan()
     assert lib().efes_plan_batch(None, one, (1 << 30) + 1, order, ctypes.byref(plan)) == ERR_ARG
     assert lib().efes_plan_batch(None, one, 1, order, ctypes.byref(plan)) == 0
+
+
+def test_mixed_config_deep_part_runs_in_rounds():
+    """configs[3] under the LPT placement model: FED4E takes the 64 MiB class on 126 CUs and the
+    GROUP4 part holds several classes (32, 16, 8 MiB: more workgroups than the 130 CUs left, so
+    it runs in rounds), which brings the step to the FED4E part's end (measured 0.884 s,
+    profiles/r02_plan_lpt/)."""
+    sizes = np.asarray([64 << 10 << i for i in range(11)], dtype=np.uint64)
+    lengths = sizes[np.random.default_rng(7).integers(0, 11, 65536)]
+    order, plan = plan_batch(lengths)
+    parts = plan.parts()
+    assert parts[0][1] == MODE_FED4E and parts[0][2]
+    assert lengths[order[0]] == 64 * MiB and lengths[order[parts[0][0] - 1]] == 64 * MiB
+    g4 = parts[1]
+    assert g4[1] == MODE_GROUP[4] and g4[2]
+    cls = set(lengths[order[parts[0][0]:parts[0][0] + g4[0]]].tolist())
+    assert len(cls) >= 2 and max(cls) == 32 * MiB
+    assert 0.85 < plan.est_seconds < 0.95
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_random_batches_give_valid_plans(seed):
+    """Any batch: parts cover it exactly, cuts fall on length boundaries, deep parts are
+    exclusive and precede the shared WIDE part, the estimate is positive."""
+    rng = np.random.default_rng(seed)
+    n = int(rng.integers(1, 40000))
+    kind = seed % 3
+    if kind == 0:
+        lengths = rng.integers(0, 1 << 26, n)
+    elif kind == 1:
+        lengths = np.exp(rng.uniform(np.log(1 << 12), np.log(1 << 26), n)).astype(np.int64)
+    else:
+        lengths = rng.choice([0, 1, 64, 4096, 1 << 20, 4 << 20, 64 << 20], n)
+    lengths = lengths.astype(np.uint64)
+    order, plan = plan_batch(lengths)
+    parts = plan.parts()
+    assert 1 <= len(parts) <= 4 and sum(p[0] for p in parts) == n
+    assert sorted(order.tolist()) == list(range(n))
+    cut = 0
+    for i, (jobs, mode, excl) in enumerate(parts):
+        assert jobs > 0
+        if mode != MODE_WIDE or i < len(parts) - 1:
+            assert excl or len(parts) == 1
+        if i < len(parts) - 1:
+            cut += jobs
+            assert lengths[order[cut - 1]] >= lengths[order[cut]]
+    assert plan.est_seconds > 0

@@ -818,6 +818,14 @@ struct FedCfg {
   static_assert(kLG > 0 && C >= 1 && C <= 3, "G in {4, 8}, 1..3 chain waves");
 };
 
+// FED4E: raw schedule words W[0..kFedHand-1] the producer hands over (it computes W[16..] of
+// them); the chain wave expands W[kFedHand..79] and adds K.
+#ifndef EFES_FED_HAND
+#define EFES_FED_HAND 16
+#endif
+constexpr int kFedHand = EFES_FED_HAND;
+static_assert(kFedHand >= 16 && kFedHand <= 80 && kFedHand % 4 == 0, "whole uint4 of raw words");
+
 struct FedSlot {
   uint4 wk[20][64];   // [word quad][lane], as PipeSlot
   uint64_t S;         // super-steps of the posted round
@@ -932,9 +940,11 @@ __device__ __forceinline__ void fed_produce(FedLDS<G, C>& L, int c, int lane, Fe
     uint32_t w[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) w[k] = bswap(cur[k]);
-    if constexpr (X) {
+    if constexpr (X) {  // the first kFedHand raw schedule words; the chain wave expands the rest
+      uint32_t r[kFedHand];
+      expand_raw<kFedHand>(w, r);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) P.wk[k][lane] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+      for (int k = 0; k < kFedHand / 4; ++k) P.wk[k][lane] = make_uint4(r[4 * k], r[4 * k + 1], r[4 * k + 2], r[4 * k + 3]);
     } else {
       uint32_t x[80];
       expand_wk(w, x);
@@ -1018,14 +1028,14 @@ __device__ void fed_consume(FedSlot& P, int lane, const DeepMsg* msgs, uint64_t 
     FED_STAT(stats[0] += __builtin_amdgcn_s_memtime() - t0;)
     uint32_t x[80];
     if constexpr (X) {
-      uint32_t w[16];
+      uint32_t w[kFedHand];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
+      for (int k = 0; k < kFedHand / 4; ++k) {
         const uint4 v = P.wk[k][lane];
         w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
       }
       lds_rel32(&P.taken, gstep + 1);  // the producer may overwrite the slot now
-      expand_wk(w, x);
+      expand_wk_from<kFedHand>(w, x);
     } else {
 #pragma unroll
       for (int k = 0; k < 20; ++k) {

@@ -128,6 +128,34 @@ __device__ __forceinline__ void expand_wk(const uint32_t (&w)[16], uint32_t (&wk
   for (int i = 60; i < 80; ++i) wk[i] = x[i] + kK3;
 }
 
+// ---- split expansion: the first N raw schedule words W[0..N-1] (N >= 16, a multiple of 4),
+// then the rest of the schedule and + K from them.
+template <int N>
+__device__ __forceinline__ void expand_raw(const uint32_t (&w)[16], uint32_t (&x)[N]) {
+#pragma unroll
+  for (int i = 0; i < 16; ++i) x[i] = w[i];
+#pragma unroll
+  for (int i = 16; i < N; ++i)
+    x[i] = rotl(__builtin_amdgcn_bitop3_b32(x[i - 3], x[i - 8], x[i - 14], 0x96) ^ x[i - 16], 1);
+}
+template <int N>
+__device__ __forceinline__ void expand_wk_from(const uint32_t (&w)[N], uint32_t (&wk)[80]) {
+  uint32_t x[80];
+#pragma unroll
+  for (int i = 0; i < N; ++i) x[i] = w[i];
+#pragma unroll
+  for (int i = N; i < 80; ++i)
+    x[i] = rotl(__builtin_amdgcn_bitop3_b32(x[i - 3], x[i - 8], x[i - 14], 0x96) ^ x[i - 16], 1);
+#pragma unroll
+  for (int i = 0; i < 20; ++i) wk[i] = x[i] + kK0;
+#pragma unroll
+  for (int i = 20; i < 40; ++i) wk[i] = x[i] + kK1;
+#pragma unroll
+  for (int i = 40; i < 60; ++i) wk[i] = x[i] + kK2;
+#pragma unroll
+  for (int i = 60; i < 80; ++i) wk[i] = x[i] + kK3;
+}
+
 // ---- compression with the schedule computed inline (16-word ring in registers).
 // Used for the few special blocks of a job (prefix/tail/padding) and by the
 // lane-per-job WIDE kernel.

@@ -902,6 +902,157 @@ Response FileReceiver::ServeHTTP(const Request& r) {  // filereceiver.go:42-127
   return w;
 }
 
+// ---- write.go ----------------------------------------------------------------------------------
+Response LocalTransport::RoundTrip(const Request& r, Error* err) {
+  *err = Error{};
+  return fr_->ServeHTTP(r);
+}
+
+namespace {
+
+struct ReadCounter : Reader {  // readcounter.go:8-27
+  Reader& r;
+  int64_t count = 0;
+  explicit ReadCounter(Reader& rr) : r(rr) {}
+  size_t Read(uint8_t* p, size_t cap, Error* err) override {
+    const size_t n = r.Read(p, cap, err);
+    count += (int64_t)n;
+    return n;
+  }
+};
+
+struct LimitReader : Reader {  // io.LimitReader
+  Reader& r;
+  int64_t left;
+  LimitReader(Reader& rr, int64_t n) : r(rr), left(n) {}
+  size_t Read(uint8_t* p, size_t cap, Error* err) override {
+    *err = Error{};
+    if (left <= 0) {
+      *err = make_error(ERR_EOF, "EOF");
+      return 0;
+    }
+    const size_t n = r.Read(p, std::min<size_t>(cap, (size_t)left), err);
+    left -= (int64_t)n;
+    return n;
+  }
+};
+
+Error check_response(const Response& w) {  // httperror.go:10-22
+  if (w.Code / 100 == 2) return Error{};
+  Error e = make_error(ERR_HTTP, std::to_string(w.Code) + ": " + w.Body);
+  e.status = w.Code;
+  return e;
+}
+
+// write.go:146-166
+Error patch(Transport& t, const std::string& path, Reader* body, int64_t offset, int64_t size, Response* w) {
+  Request r;
+  r.Method = "PATCH";
+  r.Path = path;
+  r.Headers["efes-file-offset"] = std::to_string(offset);
+  if (size > -1) r.Headers["efes-file-length"] = std::to_string(size);
+  r.Body = body;
+  Error e;
+  *w = t.RoundTrip(r, &e);
+  if (e) return e;
+  return check_response(*w);
+}
+
+Error get_offset(Transport& t, const std::string& path, int64_t* off) {  // write.go:168-178
+  Request r;
+  r.Method = "HEAD";
+  r.Path = path;
+  Error e;
+  Response w = t.RoundTrip(r, &e);
+  if (e) return e;
+  return ParseInt(w.Headers["efes-file-offset"], off);
+}
+
+Checksums checksums_from(Response& w) {  // write.go:140-145
+  return Checksums{w.Headers["efes-file-sha1"], w.Headers["efes-file-crc32"]};
+}
+
+// write.go:120-139: PATCHes of ChunkSize until the size is reached, or an empty one (then finish).
+Error send(Transport& t, const std::string& path, Reader& r, int64_t offset, int64_t size, int64_t chunk,
+           Checksums* out) {
+  ReadCounter rc(r);
+  int64_t current = offset;
+  for (;;) {
+    LimitReader chunk_reader(rc, chunk);
+    const int64_t request_offset = current;
+    Response w;
+    Error e = patch(t, path, &chunk_reader, request_offset, size, &w);
+    if (e) return e;
+    current = offset + rc.count;
+    if (current == size) {  // EOF reached: the server has deleted the offset file
+      *out = checksums_from(w);
+      return Error{};
+    }
+    if (current == request_offset) {  // nothing sent: the file was read to its end (write.go:181-188)
+      e = patch(t, path, nullptr, request_offset, request_offset, &w);
+      if (e) return e;
+      *out = checksums_from(w);
+      return Error{};
+    }
+  }
+}
+
+bool hex_decode(const std::string& h, std::string* out) {
+  if (h.size() % 2) return false;
+  out->clear();
+  for (size_t i = 0; i < h.size(); i += 2) {
+    int v = 0;
+    for (int k = 0; k < 2; ++k) {
+      const char c = h[i + k];
+      const int d = c >= '0' && c <= '9' ? c - '0' : c >= 'a' && c <= 'f' ? c - 'a' + 10 : c >= 'A' && c <= 'F' ? c - 'A' + 10 : -1;
+      if (d < 0) return false;
+      v = v * 16 + d;
+    }
+    out->push_back((char)v);
+  }
+  return true;
+}
+
+}  // namespace
+
+Error sendFile(Transport& t, efes_ctx* ctx, const std::string& path, ReadSeeker& rs, int64_t size,
+               const ClientConfig& cfg, Checksums* out) {  // write.go:68-117
+  Sha1File* sfp = nullptr;
+  Error e = Sha1File::New(&rs, ctx, &sfp);
+  if (e) return e;
+  std::unique_ptr<Sha1File> sf(sfp);
+  Checksums cs;
+  std::string remote;
+  bool first = true;
+  for (int attempt = 0;; ++attempt) {  // backoff.Retry(op, bo)
+    int64_t offset = 0;
+    e = Error{};
+    if (first) {
+      first = false;
+    } else {  // resume where the server is (write.go:84-96)
+      e = get_offset(t, path, &offset);
+      if (!e) {
+        Error se;
+        sf->Seek(offset, 0, &se);
+        e = se;
+      }
+    }
+    if (!e) e = send(t, path, *sf, offset, size, cfg.ChunkSize, &cs);
+    if (!e && !hex_decode(cs.Sha1, &remote)) e = make_error(ERR_SYNTAX, "encoding/hex: invalid byte in " + cs.Sha1);
+    if (!e) break;
+    if (e.code == ERR_HTTP && e.status == 404) return e;  // backoff.Permanent (write.go:98-100)
+    if (attempt + 1 >= cfg.MaxAttempts) return e;
+  }
+  uint8_t local[20];
+  e = sf->Sum(local);
+  if (e) return e;
+  if (remote != std::string(reinterpret_cast<char*>(local), 20))
+    return make_error(ERR_SHA1_MISMATCH, "local sha1 (" + HexEncode(local, 20) + ") does not match remote sha1 (" +
+                                             cs.Sha1 + ")");
+  *out = cs;
+  return Error{};
+}
+
 // ---- sha1file.go -------------------------------------------------------------------------------
 Error Sha1File::New(ReadSeeker* rs, efes_ctx* ctx, Sha1File** out) {  // sha1file.go:16-21
   efes_sha1* d = nullptr;

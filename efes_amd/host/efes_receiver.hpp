@@ -45,12 +45,16 @@ enum : int {
   ERR_NIL_DIGEST = -105,      // a null / missing digest in the .info JSON (Go: nil pointer, panics on Write)
   ERR_SHA1FILE = -106,        // sha1file.go:25 "missing data for sha1", :45 "seeking forward is not supported"
   ERR_SYNTAX = -107,          // strconv.ParseInt
+  ERR_HTTP = -108,            // a non-2xx response (httperror.go: ServerError / ClientError / HTTPError)
+  ERR_TRANSPORT = -109,       // the request did not complete (connection error)
+  ERR_SHA1_MISMATCH = -110,   // write.go:112-115 local vs remote SHA-1
 };
 
 struct Error {
   int code = 0;
   std::string msg;
   int64_t given = 0, required = 0;  // ERR_OFFSET_MISMATCH only
+  int status = 0;                   // ERR_HTTP: the response's status code
   explicit operator bool() const { return code != 0; }
   const std::string& str() const { return msg; }  // Go's err.Error()
 };
@@ -184,6 +188,34 @@ class FileReceiver {
   std::string dir_;
   Hasher* h_;
 };
+
+// ---- write.go: the client side of an upload (Client.sendFile) --------------------------------
+struct Checksums {  // write.go:63-66
+  std::string Sha1, CRC32;
+};
+// http.Client.Do: one request/response; *err set when the request did not complete.
+struct Transport {
+  virtual ~Transport() = default;
+  virtual Response RoundTrip(const Request& r, Error* err) = 0;
+};
+// Requests to a FileReceiver of this process (no socket).
+struct LocalTransport : Transport {
+  explicit LocalTransport(FileReceiver* fr) : fr_(fr) {}
+  Response RoundTrip(const Request& r, Error* err) override;
+
+ private:
+  FileReceiver* fr_;
+};
+struct ClientConfig {
+  int64_t ChunkSize = 50ll << 20;  // config.go:80 Client.ChunkSize (50M); one PATCH per chunk (write.go:126)
+  int MaxAttempts = 10;            // backoff.Retry's attempts (its sleeps are not modelled)
+};
+// write.go:68-117 sendFile with send (120-144), patch (146-166), getOffset (168-178) and finishFile
+// (181-188): the file read through Sha1File (hashed on the GPU while it is sent), one PATCH per
+// ChunkSize, on failure HEAD the server's offset, seek back and resend (Sha1File hashes each
+// byte once), then compare the local SHA-1 with the server's efes-file-sha1 header.
+Error sendFile(Transport& t, efes_ctx* ctx, const std::string& path, ReadSeeker& rs, int64_t size,
+               const ClientConfig& cfg, Checksums* out);
 
 // ---- sha1file.go -------------------------------------------------------------------------------
 class Sha1File : public ReadSeeker {

@@ -556,6 +556,134 @@ static void test_sha1file(const std::string& root) {
   delete sf;
 }
 
+static uint64_t rnd(uint64_t* s) {
+  *s ^= *s >> 12;
+  *s ^= *s << 25;
+  *s ^= *s >> 27;
+  return *s * 0x2545F4914F6CDD1Dull;
+}
+
+// ---- write.go sendFile against the receiver: client-side Sha1File and server-side saveFile both
+// on the GPU, with the connection failing mid-request ------------------------------------------
+// A transport that, for some PATCHes, delivers only the first k body bytes to the server (which
+// keeps them: io.Copy's error is ignored, filereceiver.go:209), loses up to `lost` more bytes in
+// flight (read from the client's Sha1File, never delivered) and reports a connection error.
+struct FlakyTransport : Transport {
+  FileReceiver* fr;
+  uint64_t s;
+  int fail_percent;
+  long failures = 0;
+  FlakyTransport(FileReceiver* f, uint64_t seed, int pct) : fr(f), s(seed | 1), fail_percent(pct) {}
+  uint64_t next() {
+    s ^= s >> 12; s ^= s << 25; s ^= s >> 27;
+    return s * 0x2545F4914F6CDD1Dull;
+  }
+  struct Cut : Reader {  // the first k bytes, then a broken connection
+    Reader& r;
+    size_t left;
+    Cut(Reader& rr, size_t k) : r(rr), left(k) {}
+    size_t Read(uint8_t* p, size_t cap, Error* err) override {
+      if (left == 0) {
+        *err = make_error(ERR_TRANSPORT, "read: connection reset by peer");
+        return 0;
+      }
+      const size_t n = r.Read(p, std::min(cap, left), err);
+      left -= n;
+      return n;
+    }
+  };
+  Response RoundTrip(const Request& r, Error* err) override {
+    *err = Error{};
+    if (r.Method != "PATCH" || !r.Body || (int)(next() % 100) >= fail_percent) return fr->ServeHTTP(r);
+    ++failures;
+    Cut cut(*r.Body, (size_t)(next() % 100000));
+    Request q = r;
+    q.Body = &cut;
+    fr->ServeHTTP(q);  // the server keeps what arrived
+    std::vector<uint8_t> lost(next() % 70000);  // in flight when the connection broke
+    Error e;
+    if (!lost.empty()) r.Body->Read(lost.data(), lost.size(), &e);
+    *err = make_error(ERR_TRANSPORT, "write: broken pipe");
+    return Response{};
+  }
+};
+
+static void expect_checksums(const Checksums& cs, const std::string& data, const char* what) {
+  uint8_t sha[20];
+  uint32_t crc;
+  oracle_hash_message(reinterpret_cast<const uint8_t*>(data.data()), data.size(), 32768, sha, &crc);
+  char c[9];
+  snprintf(c, sizeof c, "%08x", crc);
+  CHECK(cs.Sha1 == hexs(sha, 20) && cs.CRC32 == c, "%s: checksums %s %s want %s %s", what, cs.Sha1.c_str(),
+        cs.CRC32.c_str(), hexs(sha, 20).c_str(), c);
+}
+
+static void test_client_send_file(const std::string& root) {
+  {  // TestClient's content (client_test.go:158-171) through sendFile, known and unknown size
+    const std::string dir = fresh_dir(root, "client");
+    FileReceiver fr(dir, g_hasher);
+    LocalTransport t(&fr);
+    const std::string fox = "the quick brown fox jumps over the lazy dog\n";
+    for (int64_t size : {(int64_t)fox.size(), (int64_t)-1}) {
+      BytesReader rs(fox);
+      Checksums cs;
+      ClientConfig cfg;
+      cfg.ChunkSize = 16;  // three PATCHes
+      Error e = sendFile(t, g_ctx, "/0/000/1.fid", rs, size, cfg, &cs);
+      CHECK(!e, "sendFile(size %lld): %s", (long long)size, e.msg.c_str());
+      CHECK(cs.Sha1 == "5d2781d78fa5a97b7bafa849fe933dfc9dc93eba" && cs.CRC32 == "28c3debf", "fox KAT via sendFile: %s %s",
+            cs.Sha1.c_str(), cs.CRC32.c_str());
+      CHECK(slurp(dir + "/0/000/1.fid") == fox, "uploaded content");
+    }
+    BytesReader rs(fox);
+    Checksums cs;
+    FileReceiver gone(dir + "/missing", g_hasher);  // 404 is permanent (write.go:98-100)
+    struct NotFound : Transport {
+      Response RoundTrip(const Request&, Error* err) override {
+        *err = Error{};
+        Response w;
+        w.Code = 404;
+        w.Body = "tempfile does not exist\n";
+        return w;
+      }
+    } nf;
+    Error e = sendFile(nf, g_ctx, "/x.fid", rs, (int64_t)fox.size(), ClientConfig{}, &cs);
+    CHECK(e.code == ERR_HTTP && e.status == 404, "404: %d %s", e.code, e.msg.c_str());
+  }
+  // random objects over a connection that breaks in a third of the PATCHes, 8 clients at once
+  const std::string dir = fresh_dir(root, "client_flaky");
+  std::atomic<long> failures{0}, objects{0};
+  std::vector<std::thread> th;
+  for (int t = 0; t < 8; ++t)
+    th.emplace_back([&, t] {
+      FileReceiver fr(dir, g_hasher);
+      FlakyTransport ft(&fr, 0x1234567ull * (uint64_t)(t + 1), 33);
+      uint64_t s = 77 + (uint64_t)t;
+      for (int u = 0; u < 5 && !g_fail; ++u) {
+        const size_t len = (rnd(&s) % 5 == 0) ? rnd(&s) % 100 : rnd(&s) % (3u << 20);
+        std::string obj(len, '\0');
+        oracle_fill_synthetic(reinterpret_cast<uint8_t*>(&obj[0]), len, rnd(&s));
+        BytesReader rs(obj, 1 + rnd(&s) % 40000);
+        ClientConfig cfg;
+        cfg.ChunkSize = (int64_t)(1 + rnd(&s) % (1u << 20));
+        cfg.MaxAttempts = 1000;
+        const int64_t size = rnd(&s) % 3 ? (int64_t)len : -1;
+        const std::string path = "/c" + std::to_string(t) + "/" + std::to_string(u) + ".fid";
+        Checksums cs;
+        Error e = sendFile(ft, g_ctx, path, rs, size, cfg, &cs);
+        CHECK(!e, "flaky sendFile %s (len %zu, chunk %lld): %s", path.c_str(), len, (long long)cfg.ChunkSize,
+              e.msg.c_str());
+        if (!e) expect_checksums(cs, obj, path.c_str());
+        CHECK(slurp(dir + path) == obj, "%s: server file content", path.c_str());
+        ++objects;
+      }
+      failures += ft.failures;
+    });
+  for (auto& x : th) x.join();
+  printf("sendFile: %ld objects over a flaky connection, %ld broken PATCHes resumed\n", objects.load(), failures.load());
+  CHECK(failures > 10, "the flaky transport broke PATCHes");
+}
+
 // Concurrent resumable uploads through ServeHTTP, each thread with its own objects; every
 // intermediate .info is compared byte for byte with what Go would write after the same Writes.
 struct Up {
@@ -563,12 +691,6 @@ struct Up {
   long patches = 0, bytes = 0;
 };
 
-static uint64_t rnd(uint64_t* s) {
-  *s ^= *s >> 12;
-  *s ^= *s << 25;
-  *s ^= *s >> 27;
-  return *s * 0x2545F4914F6CDD1Dull;
-}
 
 static void upload_worker(const std::string& dir, int uploads, Up* a, Hasher* hasher) {
   FileReceiver fr(dir, hasher);
@@ -671,6 +793,7 @@ int main(int argc, char** argv) {
     test_file_receiver(root);
     if (!g_fail) test_save_file_errors(root);
     if (!g_fail) test_sha1file(root);
+    if (!g_fail) test_client_send_file(root);
     if (!g_fail) test_concurrent_uploads(root, threads, uploads, g_hasher, "uploads");
     delete g_hasher;
     // Several GPUs in one process: one queue per context, each PATCH on the least-loaded one

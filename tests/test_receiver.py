@@ -5,8 +5,10 @@ tests/cpp/receiver_test.cpp with every digest and every `.info` byte checked aga
 cpu: the `.info` JSON codec (json.Encoder / Decoder semantics), strconv / filepath helpers, and
      the handler paths that end before any hashing (POST, HEAD, DELETE, 400, 409).
 gpu: filereceiver_test.go's six tests with the digest headers asserted (KATs for "foo", "baz",
-     "foobar", ""), sha1file_test.go over a real file, 16 threads of resumable uploads through
-     ServeHTTP, and saveFile's error paths (broken body, vanished file, Go panic states)."""
+     "foobar", ""), sha1file_test.go over a real file, write.go's sendFile (client Sha1File and
+     server saveFile both on the GPU) over a connection that breaks PATCHes mid-body, 16 threads
+     of resumable uploads through ServeHTTP, and saveFile's error paths (broken body, vanished
+     file, Go panic states)."""
 import os
 import subprocess
 

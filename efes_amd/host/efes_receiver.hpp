@@ -4,13 +4,15 @@
 // The reference is Go (no Go toolchain in this image), so the host side that a maintainer would
 // keep in Go is mirrored here in C++, name for name, with the same argument meaning and the same
 // error behaviour, so that the reference's own tests (filereceiver_test.go, sha1file_test.go,
-// sha1_efes_test.go, crc32_efes_test.go) can be replayed against it (tests/cpp/receiver_test.cpp):
+// client_test.go's upload) can be replayed against it (tests/cpp/receiver_test.cpp):
 //
 //   fileinfo.go:10-62       FileInfo / Digest, the `<path>.info` JSON (json.Encoder / Decoder)
 //   filereceiver.go:42-127  FileReceiver.ServeHTTP (POST / HEAD / PATCH / DELETE; no socket, no DB:
 //                           the handler logic with db == nil, as filereceiver_test.go runs it)
 //   filereceiver.go:148-236 createFile, deleteFile, saveFile, OffsetMismatchError
 //   sha1file.go:9-53        Sha1File (hash-while-reading with crop-on-retry)
+//   write.go:68-188         sendFile: the client side (PATCH per ChunkSize, HEAD + seek back on
+//                           failure, local vs remote SHA-1), over a Transport
 //
 // Every byte is hashed on the GPU: saveFile streams the body through ONE upload of a batching
 // queue (efes_upload_*, hashes SHA-1 | CRC-32) -- the MultiWriter(f, CRC32, Sha1) of

@@ -944,13 +944,15 @@ Error check_response(const Response& w) {  // httperror.go:10-22
   return e;
 }
 
-// write.go:146-166
-Error patch(Transport& t, const std::string& path, Reader* body, int64_t offset, int64_t size, Response* w) {
+// write.go:154-172 (efes-drain when the client is the drainer's, client.go:21 / write.go:163-165)
+Error patch(Transport& t, const std::string& path, Reader* body, int64_t offset, int64_t size, bool drainer,
+            Response* w) {
   Request r;
   r.Method = "PATCH";
   r.Path = path;
   r.Headers["efes-file-offset"] = std::to_string(offset);
   if (size > -1) r.Headers["efes-file-length"] = std::to_string(size);
+  if (drainer) r.Headers["efes-drain"] = "true";
   r.Body = body;
   Error e;
   *w = t.RoundTrip(r, &e);
@@ -958,7 +960,7 @@ Error patch(Transport& t, const std::string& path, Reader* body, int64_t offset,
   return check_response(*w);
 }
 
-Error get_offset(Transport& t, const std::string& path, int64_t* off) {  // write.go:168-178
+Error get_offset(Transport& t, const std::string& path, int64_t* off) {  // write.go:174-185
   Request r;
   r.Method = "HEAD";
   r.Path = path;
@@ -968,28 +970,28 @@ Error get_offset(Transport& t, const std::string& path, int64_t* off) {  // writ
   return ParseInt(w.Headers["efes-file-offset"], off);
 }
 
-Checksums checksums_from(Response& w) {  // write.go:140-145
+Checksums checksums_from(Response& w) {  // write.go:146-151
   return Checksums{w.Headers["efes-file-sha1"], w.Headers["efes-file-crc32"]};
 }
 
-// write.go:120-139: PATCHes of ChunkSize until the size is reached, or an empty one (then finish).
-Error send(Transport& t, const std::string& path, Reader& r, int64_t offset, int64_t size, int64_t chunk,
+// write.go:120-144: PATCHes of ChunkSize until the size is reached, or an empty one (then finish).
+Error send(Transport& t, const std::string& path, Reader& r, int64_t offset, int64_t size, const ClientConfig& cfg,
            Checksums* out) {
   ReadCounter rc(r);
   int64_t current = offset;
   for (;;) {
-    LimitReader chunk_reader(rc, chunk);
+    LimitReader chunk_reader(rc, cfg.ChunkSize);
     const int64_t request_offset = current;
     Response w;
-    Error e = patch(t, path, &chunk_reader, request_offset, size, &w);
+    Error e = patch(t, path, &chunk_reader, request_offset, size, cfg.Drainer, &w);
     if (e) return e;
     current = offset + rc.count;
     if (current == size) {  // EOF reached: the server has deleted the offset file
       *out = checksums_from(w);
       return Error{};
     }
-    if (current == request_offset) {  // nothing sent: the file was read to its end (write.go:181-188)
-      e = patch(t, path, nullptr, request_offset, request_offset, &w);
+    if (current == request_offset) {  // nothing sent: the file was read to its end (write.go:188-195)
+      e = patch(t, path, nullptr, request_offset, request_offset, cfg.Drainer, &w);
       if (e) return e;
       *out = checksums_from(w);
       return Error{};
@@ -1037,7 +1039,7 @@ Error sendFile(Transport& t, efes_ctx* ctx, const std::string& path, ReadSeeker&
         e = se;
       }
     }
-    if (!e) e = send(t, path, *sf, offset, size, cfg.ChunkSize, &cs);
+    if (!e) e = send(t, path, *sf, offset, size, cfg, &cs);
     if (!e && !hex_decode(cs.Sha1, &remote)) e = make_error(ERR_SYNTAX, "encoding/hex: invalid byte in " + cs.Sha1);
     if (!e) break;
     if (e.code == ERR_HTTP && e.status == 404) return e;  // backoff.Permanent (write.go:98-100)

@@ -11,7 +11,7 @@
 //                           the handler logic with db == nil, as filereceiver_test.go runs it)
 //   filereceiver.go:148-236 createFile, deleteFile, saveFile, OffsetMismatchError
 //   sha1file.go:9-53        Sha1File (hash-while-reading with crop-on-retry)
-//   write.go:68-188         sendFile: the client side (PATCH per ChunkSize, HEAD + seek back on
+//   write.go:68-195         sendFile: the client side (PATCH per ChunkSize, HEAD + seek back on
 //                           failure, local vs remote SHA-1), over a Transport
 //
 // Every byte is hashed on the GPU: saveFile streams the body through ONE upload of a batching
@@ -211,9 +211,10 @@ struct LocalTransport : Transport {
 struct ClientConfig {
   int64_t ChunkSize = 50ll << 20;  // config.go:80 Client.ChunkSize (50M); one PATCH per chunk (write.go:126)
   int MaxAttempts = 10;            // backoff.Retry's attempts (its sleeps are not modelled)
+  bool Drainer = false;            // client.go:21: the drainer's client adds efes-drain: true (write.go:163-165)
 };
-// write.go:68-117 sendFile with send (120-144), patch (146-166), getOffset (168-178) and finishFile
-// (181-188): the file read through Sha1File (hashed on the GPU while it is sent), one PATCH per
+// write.go:68-117 sendFile with send (120-144), patch (154-172), getOffset (174-185) and finishFile
+// (188-195): the file read through Sha1File (hashed on the GPU while it is sent), one PATCH per
 // ChunkSize, on failure HEAD the server's offset, seek back and resend (Sha1File hashes each
 // byte once), then compare the local SHA-1 with the server's efes-file-sha1 header.
 Error sendFile(Transport& t, efes_ctx* ctx, const std::string& path, ReadSeeker& rs, int64_t size,

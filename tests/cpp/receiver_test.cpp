@@ -635,10 +635,39 @@ static void test_client_send_file(const std::string& root) {
             cs.Sha1.c_str(), cs.CRC32.c_str());
       CHECK(slurp(dir + "/0/000/1.fid") == fox, "uploaded content");
     }
+    {  // the drainer's client (drain.go:124 through write.go:163-165): every PATCH says efes-drain
+      struct Recording : Transport {
+        LocalTransport inner;
+        int patches = 0, drain = 0, heads = 0;
+        explicit Recording(FileReceiver* f) : inner(f) {}
+        Response RoundTrip(const Request& r, Error* err) override {
+          if (r.Method == "PATCH") {
+            ++patches;
+            auto it = r.Headers.find("Efes-Drain");
+            if (it != r.Headers.end() && it->second == "true") ++drain;
+          } else if (r.Method == "HEAD") {
+            ++heads;
+          }
+          return inner.RoundTrip(r, err);
+        }
+      } rec(&fr);
+      for (bool drainer : {true, false}) {
+        rec.patches = rec.drain = rec.heads = 0;
+        BytesReader rs(fox);
+        Checksums cs;
+        ClientConfig cfg;
+        cfg.ChunkSize = 10;
+        cfg.Drainer = drainer;
+        Error e = sendFile(rec, g_ctx, "/0/000/2.fid", rs, (int64_t)fox.size(), cfg, &cs);
+        CHECK(!e && cs.Sha1 == "5d2781d78fa5a97b7bafa849fe933dfc9dc93eba", "drainer=%d sendFile: %s", (int)drainer,
+              e.msg.c_str());
+        CHECK(rec.patches == 5 && rec.heads == 0 && rec.drain == (drainer ? 5 : 0),
+              "drainer=%d: %d PATCHes, %d with efes-drain, %d HEADs", (int)drainer, rec.patches, rec.drain, rec.heads);
+      }
+    }
     BytesReader rs(fox);
     Checksums cs;
-    FileReceiver gone(dir + "/missing", g_hasher);  // 404 is permanent (write.go:98-100)
-    struct NotFound : Transport {
+    struct NotFound : Transport {  // 404 is permanent (write.go:98-100)
       Response RoundTrip(const Request&, Error* err) override {
         *err = Error{};
         Response w;

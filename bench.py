@@ -253,17 +253,22 @@ def receiver_leg():
     base = "/dev/shm" if os.access("/dev/shm", os.W_OK) else tempfile.gettempdir()
     out = {}
     with tempfile.TemporaryDirectory(dir=base, prefix="efes_receiver_") as d:
-        for key, argv, size in (("receiver", ["receiver", d, "1024", "2", str(4 << 20), str(4 << 20)], 4 << 20),
+        for key, argv, size in (("receiver", ["receiver", d, "1024", "4", str(4 << 20), str(4 << 20)], 4 << 20),
+                                ("copy", ["copy", d, "1024", "4", str(4 << 20)], 0),
                                 ("sha1file", ["sha1file", d, "256", "4", str(4 << 20)], 4 << 20)):
             r = subprocess.run([exe] + argv, check=True, capture_output=True, text=True, timeout=300)
             res = json.loads(r.stdout.strip().splitlines()[-1])
+            if key == "copy":  # the same io.Copy without the digests: the host's ceiling for `receiver`
+                out["receiver"]["copy_ceiling"] = res["value"]
+                out["receiver"]["frac_of_copy"] = round(out["receiver"]["value"] / res["value"], 3)
+                continue
             src = _xorshift_bytes(size)
             want = hashlib.sha1(src).hexdigest() + ("%08x" % zlib.crc32(src) if key == "receiver" else "")
             got = res.pop("sum_sha1_crc32" if key == "receiver" else "sum_sha1")
             res["digests_match"] = got == want and res.pop("all_sums_equal")
             out[key] = res
-    out["note"] = ("host-CPU bound (file writes, staging copies, syscalls of 1024 request threads); "
-                   "not `value`")
+    out["note"] = ("receiver: saveFile with the digests on the GPU; copy_ceiling: the same requests' io.Copy "
+                   "(32 KiB reads, write, fsync) with no hashing at all, on the same host cores; not `value`")
     return out
 
 

@@ -22,6 +22,7 @@
 // slot.  No sync point issues a copy or a launch of its own.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <atomic>
@@ -50,10 +51,12 @@ struct efes_upload {
   int32_t cur = -1;              // staging chunk being filled (-1: none)
   uint64_t fill = 0;             // bytes in `cur`
   uint64_t inflight = 0;         // chunks queued or running
+  uint64_t queued = 0;           // of which still in q->pending (not in a launch yet)
   bool in_batch = false;         // has a chunk in the batch being assembled
+  bool fold_sum = false;         // Sum requested: the last queued chunk's job also writes the Sum
   std::atomic<int> latched{EFES_OK};  // first device / state error (set by the dispatcher too)
   efes_sha1_state shadow{};      // Go's x/nx/len after every Write (h from the device)
-  std::condition_variable done;  // inflight reached 0
+  std::condition_variable done;  // inflight dropped (signalled on every retired job)
 };
 
 struct Pending {
@@ -72,6 +75,7 @@ struct efes_queue {
   efes_ctx* ctx = nullptr;
   uint64_t chunk = 0;
   uint32_t nchunks = 0, max_uploads = 0;
+  uint64_t ahead = 0;              // per-upload cap on queued + running chunks while chunks are scarce
   uint8_t* h_slab = nullptr;       // pinned, device-mapped staging, nchunks x chunk
   uint8_t* z_slab = nullptr;       // the device address of h_slab: kernels read it over PCIe
   uint8_t* h_states = nullptr;     // max_uploads x kDevStateBytes, pinned + device-mapped
@@ -103,7 +107,8 @@ void efes_queue::retire(Batch& b, std::unique_lock<std::mutex>& lk) {  // mu hel
   for (const Pending& p : b.items) {
     if (p.slot != kNoChunk) free_chunks.push_back(p.slot);
     if (!ok) p.u->latched = EFES_ERR_DEVICE_FAULT;
-    if (--p.u->inflight == 0) p.u->done.notify_all();
+    --p.u->inflight;
+    p.u->done.notify_all();  // wait_idle (inflight 0) and pace (inflight < ahead)
   }
   freed.notify_all();
 }
@@ -142,6 +147,7 @@ void efes_queue::run() {
         continue;
       }
       p.u->in_batch = true;
+      --p.u->queued;
       b.items.push_back(p);
     }
     pending.swap(later);
@@ -152,14 +158,18 @@ void efes_queue::run() {
       const Pending& p = b.items[i];
       uint8_t* st = z_states + (size_t)p.u->dslot * kDevStateBytes;
       const bool sum = p.slot == kNoChunk;  // Sum: works on a copy (sha1.go:82-87), state unchanged (SUM_ONLY)
+      // The upload's last queued chunk after a Sum request: Write + Sum in one job (the kernel
+      // writes back the post-Write state and the Sum of a copy of it), one launch fewer.
+      const bool fold = !sum && p.u->fold_sum && p.u->queued == 0;
+      if (fold) p.u->fold_sum = false;
       efes_job& j = hj[i];
       j.data = sum ? nullptr : z_slab + (size_t)p.slot * chunk;
       j.length = sum ? 0 : p.len;
       j.sha1 = (p.u->hashes & EFES_HASH_SHA1) ? reinterpret_cast<efes_sha1_state*>(st) : nullptr;
       j.crc32 = (p.u->hashes & EFES_HASH_CRC32) ? reinterpret_cast<efes_crc32_state*>(st + kOffCrc) : nullptr;
-      j.sum = sum ? st + kOffSum : nullptr;
+      j.sum = sum || fold ? st + kOffSum : nullptr;
       j.status = reinterpret_cast<int32_t*>(st + kOffStatus);
-      j.flags = sum ? EFES_JOB_FINALIZE | EFES_JOB_SUM_ONLY : 0u;
+      j.flags = sum ? EFES_JOB_FINALIZE | EFES_JOB_SUM_ONLY : fold ? EFES_JOB_FINALIZE : 0u;
       j._reserved = 0;
     }
     lk.unlock();  // callers keep staging while this batch is copied and launched
@@ -180,7 +190,8 @@ void efes_queue::run() {
       for (const Pending& p : b.items) {
         if (p.slot != kNoChunk) free_chunks.push_back(p.slot);
         p.u->latched = rc;
-        if (--p.u->inflight == 0) p.u->done.notify_all();
+        --p.u->inflight;
+        p.u->done.notify_all();
       }
       freed.notify_all();
       continue;
@@ -196,10 +207,34 @@ int enqueue_current(efes_upload* u, std::unique_lock<std::mutex>&, bool even_emp
   if (u->cur < 0 || (u->fill == 0 && !even_empty)) return EFES_OK;
   q->pending.push_back(Pending{u, (uint32_t)u->cur, u->fill});
   ++u->inflight;
+  ++u->queued;
   u->cur = -1;
   u->fill = 0;
   q->work.notify_one();
   return EFES_OK;
+}
+
+// A staging chunk for `u` to fill (q->mu held): waits for a free one.
+int take_chunk(efes_upload* u, std::unique_lock<std::mutex>& lk) {
+  efes_queue* q = u->q;
+  q->freed.wait(lk, [&] { return q->fault || !q->free_chunks.empty(); });
+  if (q->fault) return u->latched = q->fault;
+  u->cur = (int32_t)q->free_chunks.back();
+  q->free_chunks.pop_back();
+  return EFES_OK;
+}
+
+// Back-pressure after a full chunk is handed over (q->mu held): while chunks are scarce, the
+// writer waits for its upload to have fewer than `ahead` chunks queued or running.  An upload
+// gains nothing from more (its chain takes one chunk per launch: one in the running launch, one
+// in the launch queued behind it, one pending for the launch after), while a fast writer that
+// grabs every free chunk leaves the other uploads nothing to put in the next launches.
+// EFES_QUEUE_AHEAD overrides kAhead (0: no per-upload cap).
+constexpr uint64_t kAhead = 3;
+void pace(efes_upload* u, std::unique_lock<std::mutex>& lk) {
+  efes_queue* q = u->q;
+  if (q->ahead && q->free_chunks.size() <= (size_t)q->max_uploads)
+    u->done.wait(lk, [&] { return q->fault || u->inflight < q->ahead; });
 }
 
 int wait_idle(efes_upload* u) {
@@ -226,6 +261,8 @@ int efes_queue_create(efes_ctx* ctx, uint64_t chunk_bytes, uint32_t max_chunks, 
   q->chunk = chunk_bytes ? (chunk_bytes + 63) & ~uint64_t(63) : (uint64_t)1 << 20;
   q->nchunks = max_chunks;
   q->max_uploads = max_uploads;
+  const char* ah = getenv("EFES_QUEUE_AHEAD");
+  q->ahead = ah && *ah ? strtoull(ah, nullptr, 10) : kAhead;
   DeviceGuard g(ctx->device);
   hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&q->h_slab), q->chunk * max_chunks, hipHostMallocMapped);
   if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void**>(&q->z_slab), q->h_slab, 0);
@@ -317,12 +354,8 @@ int efes_upload_write(efes_upload* u, const void* p, size_t n) {
     // zero-length job so the device state follows.
     std::unique_lock<std::mutex> lk(q->mu);
     enqueue_current(u, lk);  // hands a partly filled chunk over; an empty reserved one stays
-    if (u->cur < 0) {
-      q->freed.wait(lk, [&] { return !q->free_chunks.empty() || q->fault; });
-      if (q->fault) return u->latched = q->fault;
-      u->cur = (int32_t)q->free_chunks.back();
-      q->free_chunks.pop_back();
-    }
+    if (u->cur < 0)
+      if (int rc = take_chunk(u, lk)) return rc;
     u->fill = 0;
     enqueue_current(u, lk, true);
     return EFES_OK;
@@ -333,10 +366,7 @@ int efes_upload_write(efes_upload* u, const void* p, size_t n) {
   while (n > 0) {
     if (u->cur < 0) {
       std::unique_lock<std::mutex> lk(q->mu);
-      q->freed.wait(lk, [&] { return !q->free_chunks.empty() || q->fault; });  // back-pressure
-      if (q->fault) return u->latched = q->fault;
-      u->cur = (int32_t)q->free_chunks.back();
-      q->free_chunks.pop_back();
+      if (int rc = take_chunk(u, lk)) return rc;
       u->fill = 0;
     }
     const uint64_t take = std::min<uint64_t>(n, q->chunk - u->fill);
@@ -347,6 +377,7 @@ int efes_upload_write(efes_upload* u, const void* p, size_t n) {
     if (u->fill == q->chunk) {
       std::unique_lock<std::mutex> lk(q->mu);
       enqueue_current(u, lk);
+      pace(u, lk);
     }
   }
   return EFES_OK;
@@ -363,10 +394,7 @@ int efes_upload_reserve(efes_upload* u, size_t min_bytes, void** p, size_t* n) {
   }
   if (u->cur < 0) {
     std::unique_lock<std::mutex> lk(q->mu);
-    q->freed.wait(lk, [&] { return !q->free_chunks.empty() || q->fault; });  // back-pressure
-    if (q->fault) return u->latched = q->fault;
-    u->cur = (int32_t)q->free_chunks.back();
-    q->free_chunks.pop_back();
+    if (int rc = take_chunk(u, lk)) return rc;
     u->fill = 0;
   }
   *p = q->h_slab + (size_t)u->cur * q->chunk + u->fill;
@@ -387,6 +415,7 @@ int efes_upload_commit(efes_upload* u, size_t k) {
   if (u->fill == q->chunk) {
     std::unique_lock<std::mutex> lk(q->mu);
     enqueue_current(u, lk);
+    pace(u, lk);
   }
   return EFES_OK;
 }
@@ -417,13 +446,20 @@ int efes_upload_sum(efes_upload* u, uint8_t out[24]) {
   if (u->latched) return u->latched;
   efes_queue* q = u->q;
   {
-    // A zero-length FINALIZE job through the dispatcher, after the upload's staged bytes.
+    // Through the dispatcher, after the upload's staged bytes: folded into the job of its last
+    // chunk when that chunk is not in a launch yet, else a zero-length FINALIZE job.
     std::unique_lock<std::mutex> lk(q->mu);
     enqueue_current(u, lk);
-    q->pending.push_back(Pending{u, kNoChunk, 0});
-    ++u->inflight;
-    q->work.notify_one();
+    if (u->queued > 0) {  // only data chunks can be queued: a Sum returns after its job ran
+      u->fold_sum = true;
+    } else {
+      q->pending.push_back(Pending{u, kNoChunk, 0});
+      ++u->inflight;
+      ++u->queued;
+      q->work.notify_one();
+    }
     u->done.wait(lk, [&] { return u->inflight == 0; });
+    u->fold_sum = false;  // (a failed launch retires the chunk without running it)
   }
   if (u->latched) return u->latched;
   uint8_t* st = q->h_states + (size_t)u->dslot * kDevStateBytes;

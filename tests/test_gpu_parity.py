@@ -662,6 +662,47 @@ def test_upload_reserve_commit_equals_write(env, oracle):
         up.close()
 
 
+def test_upload_sum_after_queued_chunks(env, oracle):
+    """A Sum whose upload still has chunks waiting for a launch rides on the last one's job
+    (Write + Sum of a copy, one launch fewer; efes_queue.cpp): the digests, the state left
+    behind (MarshalText), a second Sum and later Writes all equal the oracle's.  A Sum that
+    fails there (Go's checkSum panic, sha1.go:107-109) leaves the state usable, as Go's does."""
+    from efes_amd._lib import Sha1State
+    from efes_amd.uploads import UploadQueue
+    efes = env["efes"]
+    data = oracle.fill_synthetic(300_000, 9).tobytes()
+    with UploadQueue(env["ctx"], chunk_bytes=4096, max_chunks=160, max_uploads=8) as q:
+        for cut in (0, 64, 4096, 3 * 4096, 3 * 4096 + 5, 100_000, 150 * 1024):
+            up = q.open()
+            o = oracle.Sha1()
+            for a in range(0, cut, 32 * 1024):  # io.Copy's buffers: several full chunks queued
+                up.write(data[a:min(a + 32 * 1024, cut)])
+            o.write(data[:cut])
+            want = (hashlib.sha1(data[:cut]).digest(), zlib.crc32(data[:cut]))
+            assert up.sums() == want
+            assert up.marshal_text()[0].decode() == o.marshal_text()
+            assert up.sums() == want  # non-destructive
+            up.write(data[cut:cut + 5000])
+            o.write(data[cut:cut + 5000])
+            assert up.sums() == (hashlib.sha1(data[:cut + 5000]).digest(), zlib.crc32(data[:cut + 5000]))
+            assert up.marshal_text()[0].decode() == o.marshal_text()
+            up.close()
+        # nx inconsistent with len (only reachable through UnmarshalText): every Sum panics in Go
+        o = oracle.Sha1()
+        o.st.nx, o.st.len = 3, 0
+        st = Sha1State()
+        st.h[:] = list(o.st.h)
+        st.nx, st.len = 3, 0
+        up = q.open(st)
+        up.write(data[:8 * 4096])
+        o.write(data[:8 * 4096])
+        with pytest.raises(efes.EfesError) as e:
+            up.sums()
+        assert e.value.code == efes.EFES_ERR_STATE
+        assert up.marshal_text()[0].decode() == o.marshal_text()
+        up.close()
+
+
 def test_upload_queue_limits(env):
     from efes_amd.uploads import UploadQueue
     efes = env["efes"]

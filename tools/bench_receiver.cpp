@@ -11,6 +11,9 @@
 //   tools/bench_receiver sha1file <dir> <threads> <files_per_thread> <file_bytes>
 //   tools/bench_receiver files    <dir> <threads> <files_per_thread> <file_bytes>   (no hashing:
 //                                 the file-system side of the receiver alone)
+//   tools/bench_receiver copy     <dir> <threads> <uploads_per_thread> <upload_bytes>  (no hashing:
+//                                 saveFile's io.Copy(f, body) alone -- 32 KiB socket reads into a
+//                                 user buffer, write, fsync, close: the receiver's host ceiling)
 //
 // Every upload carries the same bytes, so every finished upload must report the digests of a
 // reference upload made before the clock starts; each file is removed when its upload is done
@@ -18,6 +21,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <fcntl.h>
 #include <sys/statfs.h>
 #include <unistd.h>
 
@@ -93,7 +97,8 @@ Response upload(FileReceiver& fr, const std::string& path, const std::vector<uin
 
 int main(int argc, char** argv) {
   const int pinned_cpus = pin_to_cpu_quota();  // see cpu_quota.hpp
-  if (argc < 7 && !(argc >= 6 && (std::string(argv[1]) == "sha1file" || std::string(argv[1]) == "files"))) {
+  if (argc < 7 && !(argc >= 6 && (std::string(argv[1]) == "sha1file" || std::string(argv[1]) == "files" ||
+                                  std::string(argv[1]) == "copy"))) {
     fprintf(stderr,
             "usage: %s receiver <dir> <threads> <uploads_per_thread> <upload_bytes> <patch_bytes>\n"
             "       %s sha1file <dir> <threads> <files_per_thread> <file_bytes>\n",
@@ -128,7 +133,10 @@ int main(int argc, char** argv) {
       ctxs.push_back(c);
     }
     Hasher* h = nullptr;
-    Error e = Hasher::Create(ctxs, 256 << 10, 4u * (uint32_t)T + 64, (uint32_t)T, &h);
+    // staging: `per` chunks of 256 KiB per request thread (+64); EFES_BENCH_CHUNKS_PER_UPLOAD overrides
+    const char* pe = getenv("EFES_BENCH_CHUNKS_PER_UPLOAD");
+    const uint32_t per = pe && *pe ? (uint32_t)atoi(pe) : 8u;
+    Error e = Hasher::Create(ctxs, 256 << 10, per * (uint32_t)T + 64, (uint32_t)T, &h);
     if (e) {
       fprintf(stderr, "Hasher::Create: %s\n", e.msg.c_str());
       return 1;
@@ -163,10 +171,10 @@ int main(int argc, char** argv) {
     secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     delete h;
     for (size_t g = 1; g < ctxs.size(); ++g) efes_ctx_destroy(ctxs[g]);
-    printf("{\"workload\": \"receiver\", \"pinned_cpus\": %d, \"gpus\": %d, \"threads\": %d, \"uploads\": %ld, \"upload_bytes\": %zu, \"patch_bytes\": %zu, "
+    printf("{\"workload\": \"receiver\", \"pinned_cpus\": %d, \"gpus\": %d, \"staging_chunks\": %u, \"threads\": %d, \"uploads\": %ld, \"upload_bytes\": %zu, \"patch_bytes\": %zu, "
            "\"read_bytes\": 32768, \"dir_fs\": \"%s\", \"seconds\": %.4f, \"value\": %.3f, \"unit\": \"GiB/s\", "
            "\"sum_sha1_crc32\": \"%s\", \"all_sums_equal\": %s, \"errors\": %d}\n",
-           pinned_cpus, G, T, T * U, S, P, fs_name(dir), secs, (double)T * U * S / secs / (1u << 30), first.c_str(),
+           pinned_cpus, G, per * (uint32_t)T + 64, T, T * U, S, P, fs_name(dir), secs, (double)T * U * S / secs / (1u << 30), first.c_str(),
            bad ? "false" : "true", errs.load());
   } else if (mode == "files") {
     // The file-system side of the receiver alone (no hashing): per upload, create + 32 KiB
@@ -198,6 +206,42 @@ int main(int argc, char** argv) {
     secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     printf("{\"workload\": \"files\", \"pinned_cpus\": %d, \"threads\": %d, \"files\": %ld, \"file_bytes\": %zu, \"dir_fs\": \"%s\", "
            "\"seconds\": %.4f, \"value\": %.3f, \"unit\": \"GiB/s\", \"errors\": %d}\n",
+           pinned_cpus, T, T * U, S, fs_name(dir), secs, (double)T * U * S / secs / (1u << 30), errs.load());
+  } else if (mode == "copy") {
+    // saveFile without the digests (filereceiver.go:208-223 with MultiWriter(f) only): per upload,
+    // open, io.Copy from the body (32 KiB reads into a buffer, one write each), fsync, close.
+    auto t0 = std::chrono::steady_clock::now();
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t)
+      th.emplace_back([&, t] {
+        const std::string d = dir + "/copy/" + std::to_string(t);
+        if (system(("mkdir -p '" + d + "'").c_str()) != 0) {
+          ++errs;
+          return;
+        }
+        std::vector<uint8_t> buf(32 << 10);
+        for (long u = 0; u < U; ++u) {
+          const std::string path = d + "/" + std::to_string(u) + ".fid";
+          const int fd = ::open(path.c_str(), O_RDWR | O_CREAT | O_TRUNC | O_CLOEXEC, 0666);
+          if (fd < 0) {
+            ++errs;
+            return;
+          }
+          SpanReader body(src.data(), S, 32 << 10);
+          Error e;
+          for (;;) {
+            const size_t n = body.Read(buf.data(), buf.size(), &e);
+            if (n && ::write(fd, buf.data(), n) != (ssize_t)n) ++errs;
+            if (e) break;
+          }
+          if (::fsync(fd) != 0 || ::close(fd) != 0) ++errs;
+          unlink(path.c_str());
+        }
+      });
+    for (auto& x : th) x.join();
+    secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    printf("{\"workload\": \"copy\", \"pinned_cpus\": %d, \"threads\": %d, \"uploads\": %ld, \"upload_bytes\": %zu, "
+           "\"read_bytes\": 32768, \"dir_fs\": \"%s\", \"seconds\": %.4f, \"value\": %.3f, \"unit\": \"GiB/s\", \"errors\": %d}\n",
            pinned_cpus, T, T * U, S, fs_name(dir), secs, (double)T * U * S / secs / (1u << 30), errs.load());
   } else if (mode == "sha1file") {
     // One source file read by every thread U times through Sha1File (32 KiB reads).

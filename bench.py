@@ -94,6 +94,8 @@ def parse_args(argv=None):
                    help="also report 4 MiB chunks at 1K..192K in flight, one AUTO launch each (auto = N=1 only)")
     p.add_argument("--mixed-leg", choices=["auto", "on", "off"], default="auto",
                    help="also report BASELINE configs[3] (planned mixed-size batch); auto = N=1 only")
+    p.add_argument("--span-leg", choices=["auto", "on", "off"], default="auto",
+                   help="CRC-32 of one 16 GiB object (efes_crc32_span, SURVEY.md §8(f) row 4); auto = N=1 only")
     p.add_argument("--dist-backend", default="nccl", help="N>1 timing barrier/max only (no data-path collective)")
     p.add_argument("--all-ranks-on-device0", action="store_true",
                    help="rehearse the N>1 path on a 1-GPU box (use with --dist-backend gloo)")
@@ -481,6 +483,53 @@ def mixed_leg(args, rank: int, world: int, ctx, device: str, stream):
             "note": "makespan set by the 64 MiB chunks' SHA-1 chains (DESIGN.md §4 batch planner); not `value`"}
 
 
+def span_crc_leg(args, ctx, device: str, stream, gib: int = 16, reps: int = 5):
+    """CRC-32 alone of ONE object resident in HBM (efes_crc32_span, segment-
+    parallel over all CUs), against the HBM roofline; the first GiB is checked against zlib, and the
+    oracle's serial crc32.go restatement is timed on one host core over that GiB."""
+    import zlib
+
+    import torch
+
+    from oracle import oracle
+
+    n = gib << 30
+    with torch.cuda.stream(stream):
+        data = torch.empty(n, dtype=torch.uint8, device=device)
+        ctx.fill_synthetic(data.data_ptr(), n, 0x5BA4, stream.cuda_stream)
+        st = torch.zeros(1, dtype=torch.int64, device=device)
+        ctx.crc32_span(data.data_ptr(), n, st.data_ptr(), stream.cuda_stream)  # warm-up
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        stream.synchronize()
+        e0.record(stream)
+        for _ in range(reps):
+            st.zero_()
+            ctx.crc32_span(data.data_ptr(), n, st.data_ptr(), stream.cuda_stream)
+        e1.record(stream)
+        stream.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+        st.zero_()
+        ctx.crc32_span(data.data_ptr(), 1 << 30, st.data_ptr(), stream.cuda_stream)
+        stream.synchronize()
+        head = data[: 1 << 30].cpu().numpy()
+    ok = (int(st.item()) & 0xFFFFFFFF) == zlib.crc32(head)
+    o = oracle.Crc32()
+    t0 = time.perf_counter()
+    o.write(head)
+    cpu_s = time.perf_counter() - t0
+    ok = ok and o.sum32() == zlib.crc32(head)
+    del data, head
+    torch.cuda.empty_cache()
+    achieved = n / (ms * 1e-3) / 1e9
+    return {"workload": f"one {gib} GiB object, CRC-32 only (efes_crc32_span)", "bytes": n,
+            "value": round(n / (ms * 1e-3) / GiB, 1), "unit": "GiB/s", "kernel": "span_kernel",
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBPS, 4), "ms_per_call": round(ms, 3)},
+            "cpu_port_1core": {"value": round((1 << 30) / cpu_s / GiB, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+                               "sample": "oracle crc32digest.Write (slicing-by-8, crc32.go:153-169) over the first GiB"},
+            "crc_matches_zlib": ok, "note": "HIP events on the launch stream; not `value`"}
+
+
 def main(argv=None):
     args = parse_args(argv)
     import torch
@@ -595,6 +644,8 @@ def main(argv=None):
             out["concurrency"] = concurrency_leg(args, ctx, device, stream)
         if args.mixed_leg == "on" or (args.mixed_leg == "auto" and world == 1):
             out["mixed_config"] = mixed_leg(args, rank, world, ctx, device, stream)
+        if args.span_leg == "on" or (args.span_leg == "auto" and world == 1):
+            out["span_crc"] = span_crc_leg(args, ctx, device, stream)
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             threads = args.cpu_threads or host_threads()
             out["cpu_baseline"] = cpu_baseline(batches[0], data, min(n, args.cpu_max_chunks), chunk, threads,

@@ -143,6 +143,7 @@ SIGNATURES = {
     "efes_crc32_unmarshal_text": (_I, [_VP, ctypes.c_char_p, _S]),
     "efes_crc32_tables": (_I, [_VP, _S]),
     "efes_crc32_combine": (_U32, [_U32, _U32, _U64]),
+    "efes_crc32_span": (_I, [_VP, _VP, _U64, _VP, _VP]),
     "efes_sha1_state_marshal_text": (None, [_P(Sha1State), _VP]),
     "efes_sha1_state_unmarshal_text": (_I, [_P(Sha1State), ctypes.c_char_p, _S]),
     "efes_crc32_state_marshal_text": (None, [_P(Crc32State), _VP]),

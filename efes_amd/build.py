@@ -13,7 +13,7 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB_DIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIB_DIR, "libefeshash.so")
-SOURCES = ["efes_kernels.hip", "efes_api.cpp", "efes_ingest.cpp", "efes_queue.cpp", "efes_stream.cpp", "efes_plan.cpp"]
+SOURCES = ["efes_kernels.hip", "efes_crc_span.hip", "efes_api.cpp", "efes_ingest.cpp", "efes_queue.cpp", "efes_stream.cpp", "efes_plan.cpp"]
 HEADERS = ["efes_internal.hpp", "sha1_device.hpp"]
 ARCH = "gfx950"
 

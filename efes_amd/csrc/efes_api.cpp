@@ -190,6 +190,14 @@ int efes_ctx_create(int device, efes_ctx** out) {
   if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&ctx->d_tabs), tab_bytes);
   if (e == hipSuccess) e = hipMemcpy(ctx->d_tabs, host, tab_bytes, hipMemcpyHostToDevice);
   free(host);
+  if (e == hipSuccess) {
+    efes::SpanTables* span = static_cast<efes::SpanTables*>(malloc(sizeof(efes::SpanTables)));
+    if (!span) e = hipErrorOutOfMemory;
+    if (span) efes::build_span_tables(span);
+    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&ctx->d_span), sizeof(efes::SpanTables));
+    if (e == hipSuccess) e = hipMemcpy(ctx->d_span, span, sizeof(efes::SpanTables), hipMemcpyHostToDevice);
+    free(span);
+  }
   if (e != hipSuccess) {
     efes_ctx_destroy(ctx);
     return EFES_ERR_HIP;
@@ -207,6 +215,7 @@ void efes_ctx_destroy(efes_ctx* ctx) {
     for (hipStream_t sd : ctx->side)
       if (sd) (void)hipStreamSynchronize(sd);
     if (ctx->d_tabs) (void)hipFree(ctx->d_tabs);
+    if (ctx->d_span) (void)hipFree(ctx->d_span);
     if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
     for (hipEvent_t ev : ctx->ev_join)
       if (ev) (void)hipEventDestroy(ev);
@@ -296,6 +305,12 @@ int efes_fill_synthetic(efes_ctx* ctx, void* dst, size_t bytes, uint64_t seed, v
   if (!bytes) return EFES_OK;
   DeviceGuard g(ctx->device);
   return hip_err(efes::launch_fill(dst, bytes, seed, pick(ctx, stream)));
+}
+
+int efes_crc32_span(efes_ctx* ctx, const void* data, uint64_t length, efes_crc32_state* crc, void* stream) {
+  if (!ctx || !crc || (!data && length) || (reinterpret_cast<uintptr_t>(crc) & 3)) return EFES_ERR_ARG;
+  DeviceGuard g(ctx->device);
+  return hip_err(efes::launch_crc_span(data, length, &crc->crc, ctx->d_tabs, ctx->d_span, ctx->cus, pick(ctx, stream)));
 }
 
 int efes_crc32_tables(uint32_t* out, size_t nwords) {

@@ -1,0 +1,220 @@
+// efes_crc_span.hip -- CRC-32/IEEE of ONE long device buffer on the whole GPU.
+//
+// The reference's crc32digest.Write (crc32.go:76-86 -> slicingUpdate :153-169) is a serial byte
+// loop; the fused upload kernels keep it serial per chunk because SHA-1 is serial anyway.  When
+// only the CRC of one large object is wanted (an object re-checked after a drain or a copy,
+// chunks of one object on several GPUs), CRC-32 is GF(2)-linear, so any split of the bytes can be
+// CRC'd independently and merged:
+//   raw(A||B) = Z^|B| raw(A) ^ raw(B),  Z^n(v) = v * x^(8n) mod P  (reflected representation)
+// (the crc32_combine identity, efes_crc32_combine in efes_api.cpp), and Go's finalized update is
+// crc' = ~(Z^n(~crc) ^ raw(p)) (crc32.go:123,127).
+//
+// Layout of one launch over n = head + 64*nblk + rest bytes:
+//   * prep_kernel (one lane): the <= 15 head bytes up to the first 16-byte boundary byte-wise
+//     (crc32.go:125), then the state becomes ~Z^m(~crc_head) ^ raw(rest tail) with m the bytes
+//     after the head -- every bulk contribution below is then XORed into it;
+//   * span_kernel: workgroup w owns a contiguous range of 64-byte blocks; lane j takes blocks
+//     j, j+L, j+2L, ... (the wave reads 4 KiB contiguous per row), computes each block's raw CRC
+//     as the XOR of 64 independent position-table lookups (pos[p][byte], LDS) and folds it into
+//     its accumulator, acc = Z^(64L)(acc) ^ raw(block) (a byte-sliced 4 x 256 table in LDS).
+//     At the end, lane j's accumulator is advanced over the blocks of the range after its last
+//     block (one GF(2) product with lane_op[k] = x^(8*64*k)), the lanes are XOR-reduced, the sum
+//     is advanced over the bytes after the range (op[w], computed on the host) and XORed into the
+//     state with one atomic per workgroup.
+// Bound: HBM read (every byte once) against LDS table lookups (64 ds_read_b32 per 64-B block per
+// lane, random indices: bank conflicts); no SHA-1, no MFMA.  DESIGN.md §4 "span CRC".
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "efes_internal.hpp"
+
+namespace efes {
+
+constexpr uint32_t kPolyReflected = 0xedb88320u;  // crc32.go:30 IEEE, reflected
+
+// a * b mod P for polynomials in the reflected representation (bit 31 = x^0).  Branch-free, 32
+// fixed steps (uniform control flow on the device).
+__host__ __device__ inline uint32_t gf2_mulmod(uint32_t a, uint32_t b) {
+  uint32_t p = 0;
+  for (int i = 0; i < 32; ++i) {
+    p ^= b & (0u - ((a >> (31 - i)) & 1u));
+    b = (b >> 1) ^ (kPolyReflected & (0u - (b & 1u)));
+  }
+  return p;
+}
+
+// x^(8n) mod P: the operator that advances a raw CRC register over n zero bytes.
+static uint32_t xpow8n(uint64_t n) {
+  uint32_t x2n[32];            // x^(2^k) mod P; x^(2^32) = x for this primitive P, so k cycles mod 32
+  x2n[0] = 1u << 30;           // x^1
+  for (int k = 1; k < 32; ++k) x2n[k] = gf2_mulmod(x2n[k - 1], x2n[k - 1]);
+  uint32_t p = 1u << 31;       // x^0
+  for (int k = 3; n; n >>= 1, ++k)
+    if (n & 1) p = gf2_mulmod(x2n[k & 31], p);
+  return p;
+}
+
+void build_span_tables(SpanTables* t) {
+  const uint32_t row = xpow8n(64ull * kSpanLanes);  // one row of the workgroup: L blocks of 64 B
+  for (int b = 0; b < 4; ++b)
+    for (uint32_t v = 0; v < 256; ++v) t->row_shift[b][v] = gf2_mulmod(row, v << (8 * b));
+  for (int k = 0; k < kSpanLanes; ++k) t->lane_op[k] = xpow8n(64ull * (uint64_t)k);
+}
+
+struct SpanArgs {
+  const uint8_t* bulk;  // 16-byte aligned, nblk * 64 bytes
+  uint32_t* crc;        // the device state (finalized CRC), XOR target
+  const Tables* tabs;   // Tables followed by PosTables (efes_ctx_create)
+  const SpanTables* span;
+  uint64_t nblk;
+  uint32_t groups;
+  uint32_t _pad;
+  uint32_t op[kSpanMaxGroups];  // x^(8 * bytes after workgroup w's range) mod P
+};
+static_assert(sizeof(SpanArgs) <= 4096, "kernel argument segment");
+
+__global__ __launch_bounds__(64) void span_prep_kernel(const uint8_t* __restrict__ data, uint32_t head, uint32_t rest,
+                                                       const uint8_t* __restrict__ rest_ptr, uint32_t after_head_op,
+                                                       uint32_t* __restrict__ crc, const Tables* __restrict__ tabs) {
+  if (threadIdx.x != 0) return;
+  const uint32_t* t0 = tabs->slice8[0];
+  uint32_t r = ~*crc;  // crc32.go:123
+  for (uint32_t i = 0; i < head; ++i) r = t0[(r ^ data[i]) & 0xffu] ^ (r >> 8);  // crc32.go:125
+  uint32_t tail = 0;   // raw CRC of the rest bytes from a zero register
+  for (uint32_t i = 0; i < rest; ++i) tail = t0[(tail ^ rest_ptr[i]) & 0xffu] ^ (tail >> 8);
+  // ~(Z^m(r) ^ raw(bulk||rest)): the bulk's contributions are XORed in by span_kernel.
+  *crc = ~gf2_mulmod(after_head_op, r) ^ tail;
+}
+
+struct SpanLDS {
+  PosTables pos;               // 64 KiB at LDS offset 0: every pos[p][b] is a 16-bit ds_read offset
+  uint32_t row_shift[4][256];  // 4 KiB
+  uint32_t wave_sum[kSpanLanes / 64];
+};
+
+__device__ __forceinline__ void load_row(const uint8_t* src, uint32_t (&w)[16]) {
+  typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+  const __attribute__((address_space(1))) v4u* s = (const __attribute__((address_space(1))) v4u*)src;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const v4u v = s[q];
+    w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+  }
+}
+
+// Raw CRC of one 64-byte block: XOR over its 64 bytes of pos[position][byte].
+__device__ __forceinline__ uint32_t block_raw(const PosTables& P, const uint32_t (&w)[16]) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const uint32_t a = P.pos[4 * k][w[k] & 0xffu];
+    const uint32_t b = P.pos[4 * k + 1][(w[k] >> 8) & 0xffu];
+    const uint32_t c = P.pos[4 * k + 2][(w[k] >> 16) & 0xffu];
+    const uint32_t d = P.pos[4 * k + 3][w[k] >> 24];
+    r = __builtin_amdgcn_bitop3_b32(r, __builtin_amdgcn_bitop3_b32(a, b, c, 0x96), d, 0x96);
+  }
+  return r;
+}
+
+__device__ __forceinline__ uint32_t row_advance(const uint32_t (&s)[4][256], uint32_t v) {
+  return __builtin_amdgcn_bitop3_b32(s[0][v & 0xffu], s[1][(v >> 8) & 0xffu], s[2][(v >> 16) & 0xffu], 0x96) ^
+         s[3][v >> 24];
+}
+
+__global__ __launch_bounds__(kSpanLanes) void span_kernel(const SpanArgs a) {
+  __shared__ __attribute__((aligned(16))) SpanLDS L;
+  {  // tables into LDS: PosTables (64 KiB) + the row shift (4 KiB)
+    const uint4* src = reinterpret_cast<const uint4*>(a.tabs + 1);
+    uint4* dst = reinterpret_cast<uint4*>(&L.pos);
+    for (uint32_t i = threadIdx.x; i < sizeof(PosTables) / 16; i += kSpanLanes) dst[i] = src[i];
+    const uint4* s2 = reinterpret_cast<const uint4*>(a.span->row_shift);
+    uint4* d2 = reinterpret_cast<uint4*>(L.row_shift);
+    for (uint32_t i = threadIdx.x; i < sizeof(L.row_shift) / 16; i += kSpanLanes) d2[i] = s2[i];
+  }
+  const uint32_t w = blockIdx.x, j = threadIdx.x;
+  const uint64_t q = a.nblk / a.groups, r = a.nblk % a.groups;
+  const uint64_t count = q + (w < r ? 1 : 0);
+  const uint64_t start = w < r ? w * (q + 1) : r * (q + 1) + (w - r) * q;
+  const uint64_t rows = count / kSpanLanes;      // rows every lane takes part in
+  const uint32_t extra = (uint32_t)(count % kSpanLanes);  // lanes j < extra take one more block
+  const uint8_t* p = a.bulk + (start + j) * 64;
+  constexpr uint64_t kRow = 64ull * kSpanLanes;
+  __syncthreads();
+
+  uint32_t acc = 0;
+  if (rows) {
+    // two rows in flight per lane: A holds row i, B row i+1; the loads past the last row re-read
+    // the last row (clamped address, never committed)
+    uint32_t A[16], B[16];
+    load_row(p, A);
+    load_row(p + (rows > 1 ? kRow : 0), B);
+    for (uint64_t i = 0; i < rows; i += 2) {
+      const uint32_t ra = block_raw(L.pos, A);
+      load_row(p + (i + 2 < rows ? i + 2 : rows - 1) * kRow, A);
+      acc = row_advance(L.row_shift, acc) ^ ra;
+      if (i + 1 < rows) {
+        const uint32_t rb = block_raw(L.pos, B);
+        load_row(p + (i + 3 < rows ? i + 3 : rows - 1) * kRow, B);
+        acc = row_advance(L.row_shift, acc) ^ rb;
+      }
+    }
+  }
+  if (j < extra) {  // the partial last row
+    uint32_t E[16];
+    load_row(p + rows * kRow, E);
+    acc = row_advance(L.row_shift, acc) ^ block_raw(L.pos, E);
+  }
+  // Lane j's last block is followed, within the range, by (extra - 1 - j) mod L blocks.
+  const uint32_t after = (extra + kSpanLanes - 1 - j) % kSpanLanes;
+  uint32_t c = (rows || j < extra) ? gf2_mulmod(a.span->lane_op[after], acc) : 0u;
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) c ^= __shfl_xor(c, off, 64);
+  if ((j & 63) == 0) L.wave_sum[j / 64] = c;
+  __syncthreads();
+  if (j == 0) {
+    uint32_t t = 0;
+#pragma unroll
+    for (int v = 0; v < kSpanLanes / 64; ++v) t ^= L.wave_sum[v];
+    atomicXor(a.crc, gf2_mulmod(a.op[w], t));
+  }
+}
+
+hipError_t launch_crc_span(const void* data, uint64_t length, uint32_t* crc, const Tables* tabs, const SpanTables* span,
+                           int cus, hipStream_t s) {
+  const uint8_t* d = static_cast<const uint8_t*>(data);
+  const uint64_t head = length < (uint64_t)((16 - (reinterpret_cast<uintptr_t>(d) & 15)) & 15)
+                            ? length
+                            : (uint64_t)((16 - (reinterpret_cast<uintptr_t>(d) & 15)) & 15);
+  const uint64_t m = length - head, nblk = m / 64, rest = m % 64;
+  const uint8_t* bulk = d + head;
+  hipLaunchKernelGGL(span_prep_kernel, dim3(1), dim3(64), 0, s, d, (uint32_t)head, (uint32_t)rest, bulk + nblk * 64,
+                     xpow8n(m), crc, tabs);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || nblk == 0) return e;
+  // Workgroups: up to two per CU (68 KiB of LDS tables each: 16 waves per CU), at least 8 rows per
+  // lane, at most kSpanMaxGroups.
+  uint64_t groups = (nblk + 8ull * kSpanLanes - 1) / (8ull * kSpanLanes);
+  const uint64_t cap = (uint64_t)(cus > 0 ? cus : 256) * 2 < kSpanMaxGroups ? (uint64_t)(cus > 0 ? cus : 256) * 2
+                                                                          : (uint64_t)kSpanMaxGroups;
+  if (groups > cap) groups = cap;
+  if (groups == 0) groups = 1;
+  SpanArgs a{};
+  a.bulk = bulk;
+  a.crc = crc;
+  a.tabs = tabs;
+  a.span = span;
+  a.nblk = nblk;
+  a.groups = (uint32_t)groups;
+  // op[w] = x^(8 * (bytes of the ranges after w + rest)); ranges hold q+1 blocks (w < r) or q.
+  const uint64_t q = nblk / groups, r = nblk % groups;
+  const uint32_t step_q = xpow8n(64 * q), step_q1 = xpow8n(64 * (q + 1));
+  uint32_t op = xpow8n(rest);
+  for (uint64_t w = groups; w-- > 0;) {
+    a.op[w] = op;
+    op = gf2_mulmod(w < r ? step_q1 : step_q, op);  // w - 1 is followed by w's range as well
+  }
+  hipLaunchKernelGGL(span_kernel, dim3((uint32_t)groups), dim3(kSpanLanes), 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace efes

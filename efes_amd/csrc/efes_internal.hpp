@@ -59,6 +59,20 @@ hipError_t launch_group(const efes_job* jobs, uint32_t njobs, int G, const Table
 hipError_t launch_fed(const efes_job* jobs, uint32_t njobs, const Tables* tabs, hipStream_t s, bool expand);
 hipError_t launch_fill(void* dst, size_t bytes, uint64_t seed, hipStream_t s);
 
+// Span CRC (efes_crc_span.hip): CRC-32 of one long buffer on the whole GPU.  Lanes per workgroup,
+// the workgroup cap (the host passes each workgroup's combine operator as a kernel argument), and
+// the per-context operator tables: row_shift advances a raw register over one workgroup row
+// (kSpanLanes blocks of 64 B), byte-sliced; lane_op[k] = x^(8*64*k) mod P.
+constexpr int kSpanLanes = 512;
+constexpr int kSpanMaxGroups = 512;
+struct SpanTables {
+  uint32_t row_shift[4][256];
+  uint32_t lane_op[kSpanLanes];
+};
+void build_span_tables(SpanTables* t);  // host
+hipError_t launch_crc_span(const void* data, uint64_t length, uint32_t* crc, const Tables* tabs, const SpanTables* span,
+                           int cus, hipStream_t s);
+
 // Lanes per job of a grouped-DEEP mode (EFES_MODE_GROUPn -> n), 0 for other modes.
 inline int group_of_mode(int mode) {
   switch (mode) {
@@ -99,6 +113,7 @@ struct efes_ctx {
   hipStream_t part_stream(uint32_t i) const { return i < EFES_PLAN_MAX_PARTS - 1 ? side[i] : stream; }
   std::mutex plan_mu;             // one planned submit at a time uses the side streams/events
   efes::Tables* d_tabs = nullptr;
+  efes::SpanTables* d_span = nullptr;  // operators of the span CRC (efes_crc32_span)
   std::mutex mu;                  // guards the lazy creation of `digests`
   efes_queue* digests = nullptr;  // shared queue of the streaming digests (efes_stream.cpp)
 };

@@ -74,6 +74,11 @@ class Context:
         check(lib().efes_fill_synthetic(self.handle, ptr, nbytes, seed & 0xFFFFFFFFFFFFFFFF, stream),
               "efes_fill_synthetic")
 
+    def crc32_span(self, data_ptr: int, nbytes: int, crc_state_ptr: int, stream: int | None = None) -> None:
+        """efes_crc32_span: crc32.go Write (76-86) of one long device buffer into the device CRC state
+        at crc_state_ptr, segment-parallel over the whole GPU (asynchronous on `stream`)."""
+        check(lib().efes_crc32_span(self.handle, data_ptr, nbytes, crc_state_ptr, stream), "efes_crc32_span")
+
     def copy_to_host(self, dst_host: int, src_device: int, nbytes: int, stream: int | None = None) -> None:
         check(lib().efes_copy_to_host(self.handle, dst_host, src_device, nbytes, stream), "efes_copy_to_host")
 

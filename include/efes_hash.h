@@ -286,6 +286,17 @@ int efes_crc32_tables(uint32_t* out, size_t nwords);
  * devices and merged on the host; len2 may be any size (O(log len2) 32x32 GF(2) products). */
 uint32_t efes_crc32_combine(uint32_t crc1, uint32_t crc2, uint64_t len2);
 
+/* CRC-32 of ONE long device buffer on the whole GPU: the same result as
+ * crc32.go's Write (76-86) of `length` bytes at `data` (device memory, any alignment) into the
+ * device state *crc -- so chained calls compose like Writes and efes_crc32_combine merges pieces
+ * hashed on different GPUs -- but computed segment-parallel instead of byte by byte: every 64-byte
+ * block's raw CRC from position tables, merged by the GF(2)-linearity that efes_crc32_combine uses.
+ * For an object's CRC alone (a re-check after a copy or drain); uploads keep the fused SHA-1 +
+ * CRC-32 jobs above, whose speed SHA-1's serial chain sets.  Asynchronous on `stream` (NULL = the
+ * context stream); calls that share a state must be ordered on one stream. */
+int efes_crc32_span(efes_ctx* ctx, const void* data_device, uint64_t length, efes_crc32_state* crc_device,
+                    void* stream);
+
 /* Pure text codecs on plain states (no device work). */
 void efes_sha1_state_marshal_text(const efes_sha1_state* s, char out[200]);
 int efes_sha1_state_unmarshal_text(efes_sha1_state* s, const char* text, size_t n);

@@ -1,0 +1,108 @@
+"""GPU parity of the span CRC (efes_crc32_span): CRC-32 of one long device
+buffer computed segment-parallel over the whole GPU must equal crc32.go's serial Write
+(crc32.go:76-86) of the same bytes -- the oracle's C restatement for small cases, zlib.crc32 (the
+same IEEE algorithm, pinned against the oracle in test_oracle.py) at sizes the oracle would take
+long on, and size-independent properties (chained calls = one call, pieces merged by
+efes_crc32_combine = one call) at full size.  Bit-exact."""
+import random
+import zlib
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def env():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from efes_amd import hashing
+    from oracle import oracle
+    return dict(torch=torch, hashing=hashing, ctx=hashing.default_context(0), oracle=oracle)
+
+
+def _span(env, buf, off: int, n: int, crc_in: int = 0) -> int:
+    """efes_crc32_span of buf[off:off+n] into a device state holding crc_in."""
+    torch = env["torch"]
+    st = torch.tensor([crc_in], dtype=torch.int64, device="cuda:0")  # the state is its low 4 bytes
+    env["ctx"].crc32_span(buf.data_ptr() + off, n, st.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    return int(st.item()) & 0xFFFFFFFF
+
+
+def _device_bytes(env, nbytes: int, seed: int):
+    torch = env["torch"]
+    buf = torch.empty(nbytes, dtype=torch.uint8, device="cuda:0")
+    env["ctx"].fill_synthetic(buf.data_ptr(), nbytes - nbytes % 8, seed, torch.cuda.current_stream().cuda_stream)
+    if nbytes % 8:
+        buf[nbytes - nbytes % 8:] = 0x5A
+    torch.cuda.synchronize()
+    return buf
+
+
+# lengths around every boundary of the decomposition: the 16-byte head, 64-byte blocks, one
+# workgroup row (512 blocks = 32 KiB), several rows, ragged workgroup ranges
+LENGTHS = [0, 1, 15, 16, 17, 63, 64, 65, 127, 128, 1000, 4095, 4096, 4097, 32767, 32768, 32769,
+           65536 + 64 * 7 + 5, 262144 + 3, (1 << 20) + 13, 3 * (1 << 20) - 1]
+
+
+def test_span_matches_oracle_small(env):
+    """Every length and misalignment 0..15 against the oracle's crc32digest, from fresh and mid-stream states."""
+    oracle = env["oracle"]
+    total = max(LENGTHS) + 64
+    buf = _device_bytes(env, total, 0x5BA7)
+    host = buf.cpu().numpy()
+    rng = random.Random(11)
+    for n in LENGTHS:
+        for off in (0, 1, 7, 15) if n > 4096 else range(16):
+            o = oracle.Crc32()
+            crc_in = rng.choice([0, 0xFFFFFFFF, rng.getrandbits(32)])
+            o.st.crc = crc_in
+            o.write(host[off:off + n].tobytes())
+            got = _span(env, buf, off, n, crc_in)
+            assert got == o.sum32(), (n, off, hex(crc_in), hex(got), hex(o.sum32()))
+
+
+def test_span_matches_zlib_many_workgroups(env):
+    """Sizes that spread over hundreds of workgroups with ragged ranges (nblk not a multiple of the
+    workgroup count), misaligned, against zlib."""
+    buf = _device_bytes(env, (300 << 20) + 4096, 0xC0FFEE)
+    host = buf.cpu().numpy()
+    for off, n in [(0, 300 << 20), (3, (300 << 20) - 7), (9, (137 << 20) + 12345), (0, (64 << 20) + 64 * 513 + 1)]:
+        exp = zlib.crc32(host[off:off + n])
+        assert _span(env, buf, off, n) == exp, (off, n)
+
+
+def test_span_chained_and_combined_full_size(env):
+    """4 GiB + 5 bytes: one call == random pieces chained through one state == pieces on separate
+    states merged with efes_crc32_combine (the multi-GPU gather); zlib at the end."""
+    n = (4 << 30) + 5
+    buf = _device_bytes(env, n, 0x10B)
+    whole = _span(env, buf, 0, n)
+    rng = random.Random(5)
+    cuts = sorted(rng.sample(range(1, n), 6))
+    bounds = [0] + cuts + [n]
+    chained = 0
+    merged = None
+    for a, b in zip(bounds, bounds[1:]):
+        chained = _span(env, buf, a, b - a, chained)
+        part = _span(env, buf, a, b - a)
+        merged = part if merged is None else env["hashing"].crc32_combine(merged, part, b - a)
+    assert chained == whole and merged == whole
+    # zlib over the host copy, in 1 GiB pieces
+    crc = 0
+    for a in range(0, n, 1 << 30):
+        crc = zlib.crc32(buf[a:min(n, a + (1 << 30))].cpu().numpy(), crc)
+    assert whole == crc
+
+
+def test_span_zero_bytes_and_constant_data(env):
+    """All-zero and all-0xFF buffers (the CRC's fixed-pattern cases), 16 MiB + 3, against zlib."""
+    torch = env["torch"]
+    n = (16 << 20) + 3
+    for v in (0, 0xFF):
+        buf = torch.full((n,), v, dtype=torch.uint8, device="cuda:0")
+        assert _span(env, buf, 0, n) == zlib.crc32(bytes([v]) * n)
+        assert _span(env, buf, 1, n - 1, 0x12345678) == zlib.crc32(bytes([v]) * (n - 1), 0x12345678)

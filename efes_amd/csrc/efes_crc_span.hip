@@ -55,18 +55,18 @@ static uint32_t xpow8n(uint64_t n) {
 }
 
 void build_span_tables(SpanTables* t) {
-  const uint32_t row = xpow8n(64ull * kSpanLanes);  // one row of the workgroup: L blocks of 64 B
+  const uint32_t row = xpow8n((uint64_t)kSpanLine * kSpanLanes);  // one workgroup row: L lines
   for (int b = 0; b < 4; ++b)
     for (uint32_t v = 0; v < 256; ++v) t->row_shift[b][v] = gf2_mulmod(row, v << (8 * b));
-  for (int k = 0; k < kSpanLanes; ++k) t->lane_op[k] = xpow8n(64ull * (uint64_t)k);
+  for (int k = 0; k < kSpanLanes; ++k) t->lane_op[k] = xpow8n((uint64_t)kSpanLine * (uint64_t)k);
 }
 
 struct SpanArgs {
-  const uint8_t* bulk;  // 16-byte aligned, nblk * 64 bytes
+  const uint8_t* bulk;  // 16-byte aligned, nline * kSpanLine bytes
   uint32_t* crc;        // the device state (finalized CRC), XOR target
-  const Tables* tabs;   // Tables followed by PosTables (efes_ctx_create)
+  const Tables* tabs;   // slicing-by-8 tables (crc32.go:138-149)
   const SpanTables* span;
-  uint64_t nblk;
+  uint64_t nline;
   uint32_t groups;
   uint32_t _pad;
   uint32_t op[kSpanMaxGroups];  // x^(8 * bytes after workgroup w's range) mod P
@@ -86,34 +86,45 @@ __global__ __launch_bounds__(64) void span_prep_kernel(const uint8_t* __restrict
   *crc = ~gf2_mulmod(after_head_op, r) ^ tail;
 }
 
+// LDS: the eight slicing-by-8 tables with every entry stored kSpanCopies times side by side
+// (word t*256*C + e*C + c), lane j reading copy j % C: a ds_read_b32 serves its 32-lane groups
+// with at most 2-way bank conflicts (lanes j and j+16 of a group share a copy) instead of the
+// ~3.5-way of random indices into one table; the row shift (4 lookups per line) keeps one copy.
+constexpr int kSpanCopies = 16;
 struct SpanLDS {
-  PosTables pos;               // 64 KiB at LDS offset 0: every pos[p][b] is a 16-bit ds_read offset
-  uint32_t row_shift[4][256];  // 4 KiB
+  uint32_t slice[8][256][kSpanCopies];  // 128 KiB
+  uint32_t row_shift[4][256];           // 4 KiB
   uint32_t wave_sum[kSpanLanes / 64];
 };
 
-__device__ __forceinline__ void load_row(const uint8_t* src, uint32_t (&w)[16]) {
+constexpr int kLineWords = kSpanLine / 4;
+
+__device__ __forceinline__ void load_line(const uint8_t* src, uint32_t (&w)[kLineWords]) {
   typedef uint32_t v4u __attribute__((ext_vector_type(4)));
   const __attribute__((address_space(1))) v4u* s = (const __attribute__((address_space(1))) v4u*)src;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  for (int q = 0; q < kLineWords / 4; ++q) {
     const v4u v = s[q];
     w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
   }
 }
 
-// Raw CRC of one 64-byte block: XOR over its 64 bytes of pos[position][byte].
-__device__ __forceinline__ uint32_t block_raw(const PosTables& P, const uint32_t (&w)[16]) {
-  uint32_t r = 0;
+// Raw CRC (from a zero register) of one line: slicing-by-8 as crc32.go:157-161, the lookups into
+// this lane's copy of the tables.  lo / hi: &slice[0][0][c] and &slice[4][0][c] (byte addresses
+// within 16-bit ds_read offsets of their base).
+__device__ __forceinline__ uint32_t line_raw(const uint32_t* lo, const uint32_t* hi, const uint32_t (&w)[kLineWords]) {
+  constexpr int E = kSpanCopies, T = 256 * kSpanCopies;  // entry and table strides in words
+  uint32_t crc = 0;
 #pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    const uint32_t a = P.pos[4 * k][w[k] & 0xffu];
-    const uint32_t b = P.pos[4 * k + 1][(w[k] >> 8) & 0xffu];
-    const uint32_t c = P.pos[4 * k + 2][(w[k] >> 16) & 0xffu];
-    const uint32_t d = P.pos[4 * k + 3][w[k] >> 24];
-    r = __builtin_amdgcn_bitop3_b32(r, __builtin_amdgcn_bitop3_b32(a, b, c, 0x96), d, 0x96);
+  for (int s = 0; s < kLineWords / 2; ++s) {
+    const uint32_t x = crc ^ w[2 * s], y = w[2 * s + 1];
+    const uint32_t a = __builtin_amdgcn_bitop3_b32(lo[0 * T + E * (y >> 24)], lo[1 * T + E * ((y >> 16) & 0xffu)],
+                                                   lo[2 * T + E * ((y >> 8) & 0xffu)], 0x96);
+    const uint32_t b = __builtin_amdgcn_bitop3_b32(lo[3 * T + E * (y & 0xffu)], hi[0 * T + E * (x >> 24)],
+                                                   hi[1 * T + E * ((x >> 16) & 0xffu)], 0x96);
+    crc = __builtin_amdgcn_bitop3_b32(a, b, hi[2 * T + E * ((x >> 8) & 0xffu)] ^ hi[3 * T + E * (x & 0xffu)], 0x96);
   }
-  return r;
+  return crc;
 }
 
 __device__ __forceinline__ uint32_t row_advance(const uint32_t (&s)[4][256], uint32_t v) {
@@ -123,48 +134,53 @@ __device__ __forceinline__ uint32_t row_advance(const uint32_t (&s)[4][256], uin
 
 __global__ __launch_bounds__(kSpanLanes) void span_kernel(const SpanArgs a) {
   __shared__ __attribute__((aligned(16))) SpanLDS L;
-  {  // tables into LDS: PosTables (64 KiB) + the row shift (4 KiB)
-    const uint4* src = reinterpret_cast<const uint4*>(a.tabs + 1);
-    uint4* dst = reinterpret_cast<uint4*>(&L.pos);
-    for (uint32_t i = threadIdx.x; i < sizeof(PosTables) / 16; i += kSpanLanes) dst[i] = src[i];
+  {  // tables into LDS: each slicing entry kSpanCopies times (4 per ds_write_b128), the row shift once
+    const uint32_t* src = &a.tabs->slice8[0][0];
+    uint4* dst = reinterpret_cast<uint4*>(&L.slice[0][0][0]);
+    for (uint32_t i = threadIdx.x; i < 8 * 256 * kSpanCopies / 4; i += kSpanLanes) {
+      const uint32_t v = src[i / (kSpanCopies / 4)];
+      dst[i] = make_uint4(v, v, v, v);
+    }
     const uint4* s2 = reinterpret_cast<const uint4*>(a.span->row_shift);
     uint4* d2 = reinterpret_cast<uint4*>(L.row_shift);
     for (uint32_t i = threadIdx.x; i < sizeof(L.row_shift) / 16; i += kSpanLanes) d2[i] = s2[i];
   }
   const uint32_t w = blockIdx.x, j = threadIdx.x;
-  const uint64_t q = a.nblk / a.groups, r = a.nblk % a.groups;
+  const uint64_t q = a.nline / a.groups, r = a.nline % a.groups;
   const uint64_t count = q + (w < r ? 1 : 0);
   const uint64_t start = w < r ? w * (q + 1) : r * (q + 1) + (w - r) * q;
-  const uint64_t rows = count / kSpanLanes;      // rows every lane takes part in
-  const uint32_t extra = (uint32_t)(count % kSpanLanes);  // lanes j < extra take one more block
-  const uint8_t* p = a.bulk + (start + j) * 64;
-  constexpr uint64_t kRow = 64ull * kSpanLanes;
+  const uint64_t rows = count / kSpanLanes;               // rows every lane takes part in
+  const uint32_t extra = (uint32_t)(count % kSpanLanes);  // lanes j < extra take one more line
+  const uint8_t* p = a.bulk + (start + j) * kSpanLine;
+  constexpr uint64_t kRow = (uint64_t)kSpanLine * kSpanLanes;
+  const uint32_t* lo = &L.slice[0][0][j % kSpanCopies];
+  const uint32_t* hi = &L.slice[4][0][j % kSpanCopies];
   __syncthreads();
 
   uint32_t acc = 0;
   if (rows) {
-    // two rows in flight per lane: A holds row i, B row i+1; the loads past the last row re-read
+    // two lines in flight per lane: A holds row i, B row i+1; the loads past the last row re-read
     // the last row (clamped address, never committed)
-    uint32_t A[16], B[16];
-    load_row(p, A);
-    load_row(p + (rows > 1 ? kRow : 0), B);
+    uint32_t A[kLineWords], B[kLineWords];
+    load_line(p, A);
+    load_line(p + (rows > 1 ? kRow : 0), B);
     for (uint64_t i = 0; i < rows; i += 2) {
-      const uint32_t ra = block_raw(L.pos, A);
-      load_row(p + (i + 2 < rows ? i + 2 : rows - 1) * kRow, A);
+      const uint32_t ra = line_raw(lo, hi, A);
+      load_line(p + (i + 2 < rows ? i + 2 : rows - 1) * kRow, A);
       acc = row_advance(L.row_shift, acc) ^ ra;
       if (i + 1 < rows) {
-        const uint32_t rb = block_raw(L.pos, B);
-        load_row(p + (i + 3 < rows ? i + 3 : rows - 1) * kRow, B);
+        const uint32_t rb = line_raw(lo, hi, B);
+        load_line(p + (i + 3 < rows ? i + 3 : rows - 1) * kRow, B);
         acc = row_advance(L.row_shift, acc) ^ rb;
       }
     }
   }
   if (j < extra) {  // the partial last row
-    uint32_t E[16];
-    load_row(p + rows * kRow, E);
-    acc = row_advance(L.row_shift, acc) ^ block_raw(L.pos, E);
+    uint32_t E[kLineWords];
+    load_line(p + rows * kRow, E);
+    acc = row_advance(L.row_shift, acc) ^ line_raw(lo, hi, E);
   }
-  // Lane j's last block is followed, within the range, by (extra - 1 - j) mod L blocks.
+  // Lane j's last line is followed, within the range, by (extra - 1 - j) mod L lines.
   const uint32_t after = (extra + kSpanLanes - 1 - j) % kSpanLanes;
   uint32_t c = (rows || j < extra) ? gf2_mulmod(a.span->lane_op[after], acc) : 0u;
 #pragma unroll
@@ -185,17 +201,16 @@ hipError_t launch_crc_span(const void* data, uint64_t length, uint32_t* crc, con
   const uint64_t head = length < (uint64_t)((16 - (reinterpret_cast<uintptr_t>(d) & 15)) & 15)
                             ? length
                             : (uint64_t)((16 - (reinterpret_cast<uintptr_t>(d) & 15)) & 15);
-  const uint64_t m = length - head, nblk = m / 64, rest = m % 64;
+  const uint64_t m = length - head, nline = m / kSpanLine, rest = m % kSpanLine;
   const uint8_t* bulk = d + head;
-  hipLaunchKernelGGL(span_prep_kernel, dim3(1), dim3(64), 0, s, d, (uint32_t)head, (uint32_t)rest, bulk + nblk * 64,
-                     xpow8n(m), crc, tabs);
+  hipLaunchKernelGGL(span_prep_kernel, dim3(1), dim3(64), 0, s, d, (uint32_t)head, (uint32_t)rest,
+                     bulk + nline * kSpanLine, xpow8n(m), crc, tabs);
   hipError_t e = hipGetLastError();
-  if (e != hipSuccess || nblk == 0) return e;
-  // Workgroups: up to two per CU (68 KiB of LDS tables each: 16 waves per CU), at least 8 rows per
-  // lane, at most kSpanMaxGroups.
-  uint64_t groups = (nblk + 8ull * kSpanLanes - 1) / (8ull * kSpanLanes);
-  const uint64_t cap = (uint64_t)(cus > 0 ? cus : 256) * 2 < kSpanMaxGroups ? (uint64_t)(cus > 0 ? cus : 256) * 2
-                                                                          : (uint64_t)kSpanMaxGroups;
+  if (e != hipSuccess || nline == 0) return e;
+  // Workgroups: one per CU (132 KiB of LDS tables, 16 waves), at least 4 rows per lane.
+  uint64_t groups = (nline + 4ull * kSpanLanes - 1) / (4ull * kSpanLanes);
+  const uint64_t cap = (uint64_t)(cus > 0 ? cus : 256) < kSpanMaxGroups ? (uint64_t)(cus > 0 ? cus : 256)
+                                                                      : (uint64_t)kSpanMaxGroups;
   if (groups > cap) groups = cap;
   if (groups == 0) groups = 1;
   SpanArgs a{};
@@ -203,11 +218,11 @@ hipError_t launch_crc_span(const void* data, uint64_t length, uint32_t* crc, con
   a.crc = crc;
   a.tabs = tabs;
   a.span = span;
-  a.nblk = nblk;
+  a.nline = nline;
   a.groups = (uint32_t)groups;
-  // op[w] = x^(8 * (bytes of the ranges after w + rest)); ranges hold q+1 blocks (w < r) or q.
-  const uint64_t q = nblk / groups, r = nblk % groups;
-  const uint32_t step_q = xpow8n(64 * q), step_q1 = xpow8n(64 * (q + 1));
+  // op[w] = x^(8 * (bytes of the ranges after w + rest)); ranges hold q+1 lines (w < r) or q.
+  const uint64_t q = nline / groups, r = nline % groups;
+  const uint32_t step_q = xpow8n(kSpanLine * q), step_q1 = xpow8n(kSpanLine * (q + 1));
   uint32_t op = xpow8n(rest);
   for (uint64_t w = groups; w-- > 0;) {
     a.op[w] = op;

@@ -59,11 +59,13 @@ hipError_t launch_group(const efes_job* jobs, uint32_t njobs, int G, const Table
 hipError_t launch_fed(const efes_job* jobs, uint32_t njobs, const Tables* tabs, hipStream_t s, bool expand);
 hipError_t launch_fill(void* dst, size_t bytes, uint64_t seed, hipStream_t s);
 
-// Span CRC (efes_crc_span.hip): CRC-32 of one long buffer on the whole GPU.  Lanes per workgroup,
-// the workgroup cap (the host passes each workgroup's combine operator as a kernel argument), and
-// the per-context operator tables: row_shift advances a raw register over one workgroup row
-// (kSpanLanes blocks of 64 B), byte-sliced; lane_op[k] = x^(8*64*k) mod P.
-constexpr int kSpanLanes = 512;
+// Span CRC (efes_crc_span.hip): CRC-32 of one long buffer on the whole GPU.  Bytes per lane per
+// row (one 128-B cache line), lanes per workgroup, the workgroup cap (the host passes each
+// workgroup's combine operator as a kernel argument), and the per-context operator tables:
+// row_shift advances a raw register over one workgroup row (kSpanLanes lines), byte-sliced;
+// lane_op[k] = x^(8*kSpanLine*k) mod P.
+constexpr int kSpanLine = 128;
+constexpr int kSpanLanes = 1024;
 constexpr int kSpanMaxGroups = 512;
 struct SpanTables {
   uint32_t row_shift[4][256];

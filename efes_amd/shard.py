@@ -76,3 +76,48 @@ def gather_results(local: dict[int, tuple[str, int]]) -> dict[int, tuple[str, in
             raise RuntimeError(f"objects hashed on two ranks: {sorted(dup)[:5]}")
         out.update(p)
     return out
+
+
+# ---- one object's CRC-32 over several GPUs (SURVEY.md §8(e)/(f) row 4) ------------------------
+# SHA-1 of an object cannot be split (one chain), but CRC-32 can: rank r spans piece r of the
+# object from a zero state (efes_crc32_span on its GPU), the ranks exchange their 4-byte CRCs and
+# piece lengths (one all_gather: the only data-path collective, 16 bytes per rank), and every rank
+# folds them in piece order with the GF(2) combine of crc32.go's linearity (efes_crc32_combine).
+
+
+def piece_bounds(length: int, world: int, align: int = 4096) -> list[tuple[int, int]]:
+    """[(offset, length)] of `world` contiguous pieces covering [0, length), piece starts on
+    `align`-byte boundaries (the last piece takes the remainder; pieces may be empty)."""
+    if world < 1:
+        raise ValueError("world must be >= 1")
+    per = -(-length // world)
+    per = -(-per // align) * align if per else 0
+    out = []
+    for r in range(world):
+        a = min(length, r * per)
+        out.append((a, min(length, a + per) - a))
+    return out
+
+
+def combine_piece_crcs(pieces, crc_in: int = 0) -> int:
+    """crc32.go Write of the concatenated pieces into a state holding crc_in, from each piece's
+    CRC from a zero state: [(crc, length)] in object order."""
+    from efes_amd.hashing import crc32_combine
+
+    crc = crc_in & 0xFFFFFFFF
+    for c, n in pieces:
+        crc = crc32_combine(crc, int(c), int(n))
+    return crc
+
+
+def gather_piece_crcs(crc: int, length: int, device=None) -> list[tuple[int, int]]:
+    """Every rank's (crc, length), in rank order (all_gather of 16 bytes per rank)."""
+    import torch
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return [(crc & 0xFFFFFFFF, length)]
+    mine = torch.tensor([crc & 0xFFFFFFFF, length], dtype=torch.int64, device=device)
+    parts = [torch.empty_like(mine) for _ in range(dist.get_world_size())]
+    dist.all_gather(parts, mine)
+    return [(int(p[0].item()), int(p[1].item())) for p in parts]

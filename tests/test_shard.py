@@ -12,7 +12,8 @@ import zlib
 import numpy as np
 import pytest
 
-from efes_amd.shard import gather_results, loads, lpt_assign, max_over_ranks
+from efes_amd.shard import (combine_piece_crcs, gather_piece_crcs, gather_results, loads, lpt_assign,
+                            max_over_ranks, piece_bounds)
 
 
 def test_lpt_every_object_once_and_balanced():
@@ -94,3 +95,52 @@ def test_two_rank_gloo_sharding_matches_single_process():
     assert sum(counts) == len(objs) and min(counts) > 0
 
 
+def test_piece_bounds_cover_the_object():
+    for length in (0, 1, 4095, 4096, 4097, 10 << 20, (10 << 20) + 3):
+        for world in (1, 2, 3, 8):
+            b = piece_bounds(length, world)
+            assert len(b) == world and sum(n for _, n in b) == length
+            assert all(a % 4096 == 0 or n == 0 for a, n in b)
+            assert all(b[i][0] + b[i][1] == b[i + 1][0] or b[i + 1][1] == 0 for i in range(world - 1))
+
+
+def test_combine_piece_crcs_equals_one_pass():
+    """Pieces CRC'd from zero states and folded in order == crc32.go over the whole (zlib), from
+    any starting state."""
+    rng = np.random.default_rng(9)
+    data = rng.integers(0, 256, 1_000_003, dtype=np.uint8).tobytes()
+    for world in (1, 2, 5, 8):
+        pieces = [(zlib.crc32(data[a:a + n]), n) for a, n in piece_bounds(len(data), world, align=64)]
+        assert combine_piece_crcs(pieces) == zlib.crc32(data)
+        assert combine_piece_crcs(pieces, 0xDEADBEEF) == zlib.crc32(data, 0xDEADBEEF)
+
+
+def _crc_worker(rank, world, port, q):
+    import torch.distributed as dist
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        data = np.random.default_rng(21).integers(0, 256, 3_000_017, dtype=np.uint8).tobytes()
+        a, n = piece_bounds(len(data), world)[rank]
+        pieces = gather_piece_crcs(zlib.crc32(data[a:a + n]), n)  # the rank's GPU would span its piece
+        q.put((rank, combine_piece_crcs(pieces)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_gloo_object_crc_matches_single_pass():
+    """One object's CRC over two ranks: each CRCs its piece, all_gather of (crc, len), fold."""
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_crc_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    data = np.random.default_rng(21).integers(0, 256, 3_000_017, dtype=np.uint8).tobytes()
+    assert got == {0: zlib.crc32(data), 1: zlib.crc32(data)}

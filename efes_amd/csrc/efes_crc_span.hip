@@ -9,22 +9,23 @@
 // (the crc32_combine identity, efes_crc32_combine in efes_api.cpp), and Go's finalized update is
 // crc' = ~(Z^n(~crc) ^ raw(p)) (crc32.go:123,127).
 //
-// Layout of one launch over n = head + 64*nblk + rest bytes:
-//   * prep_kernel (one lane): the <= 15 head bytes up to the first 16-byte boundary byte-wise
-//     (crc32.go:125), then the state becomes ~Z^m(~crc_head) ^ raw(rest tail) with m the bytes
-//     after the head -- every bulk contribution below is then XORed into it;
-//   * span_kernel: workgroup w owns a contiguous range of 64-byte blocks; lane j takes blocks
-//     j, j+L, j+2L, ... (the wave reads 4 KiB contiguous per row), computes each block's raw CRC
-//     as the XOR of 64 independent position-table lookups (pos[p][byte], LDS) and folds it into
-//     its accumulator, acc = Z^(64L)(acc) ^ raw(block) (a byte-sliced 4 x 256 table in LDS).
-//     At the end, lane j's accumulator is advanced over the blocks of the range after its last
-//     block (one GF(2) product with lane_op[k] = x^(8*64*k)), the lanes are XOR-reduced, the sum
-//     is advanced over the bytes after the range (op[w], computed on the host) and XORed into the
-//     state with one atomic per workgroup.
-// Bound: HBM read (every byte once) against LDS table lookups (64 ds_read_b32 per 64-B block per
-// lane, random indices: bank conflicts); no SHA-1, no MFMA.  DESIGN.md §4 "span CRC".
+// Layout of one launch over n = head + 128*nline + rest bytes:
+//   * span_prep_kernel (one lane): the <= 15 head bytes up to the first 16-byte boundary and the
+//     < 128 rest bytes byte-wise (crc32.go:125); the state becomes ~Z^m(~crc_head) ^ raw(rest)
+//     with m the bytes after the head -- every bulk contribution below is then XORed into it;
+//   * span_kernel: workgroup w owns a contiguous range of 128-byte lines; lane j takes lines j,
+//     j+L, j+2L, ... (a wave reads 8 KiB per row), computes each line's raw CRC by slicing-by-4
+//     from lane-private copies of the tables in LDS (no bank conflicts, one v_perm per lookup
+//     address) and folds it into its accumulator, acc = Z^(128L)(acc) ^ raw(line) (a byte-sliced
+//     4 x 256 table).  At the end, lane j's accumulator is advanced over the lines of the range
+//     after its last line (one GF(2) product with lane_op[k] = x^(8*128*k)), the lanes are
+//     XOR-reduced, the sum is advanced over the bytes after the range (op[w], computed on the
+//     host) and XORed into the state with one atomic per workgroup.
+// Bound: HBM read (every byte once); measured at ~85 % of a pure read kernel (DESIGN.md §4 "Span
+// CRC").  No SHA-1, no MFMA.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "efes_internal.hpp"
 
@@ -72,6 +73,7 @@ struct SpanArgs {
   uint32_t op[kSpanMaxGroups];  // x^(8 * bytes after workgroup w's range) mod P
 };
 static_assert(sizeof(SpanArgs) <= 4096, "kernel argument segment");
+static_assert(kSpanLine % 4 == 0, "whole words per line");
 
 __global__ __launch_bounds__(64) void span_prep_kernel(const uint8_t* __restrict__ data, uint32_t head, uint32_t rest,
                                                        const uint8_t* __restrict__ rest_ptr, uint32_t after_head_op,
@@ -86,18 +88,39 @@ __global__ __launch_bounds__(64) void span_prep_kernel(const uint8_t* __restrict
   *crc = ~gf2_mulmod(after_head_op, r) ^ tail;
 }
 
-// LDS: the eight slicing-by-8 tables with every entry stored kSpanCopies times side by side
-// (word t*256*C + e*C + c), lane j reading copy j % C: a ds_read_b32 serves its 32-lane groups
-// with at most 2-way bank conflicts (lanes j and j+16 of a group share a copy) instead of the
-// ~3.5-way of random indices into one table; the row shift (4 lookups per line) keeps one copy.
-constexpr int kSpanCopies = 16;
+// LDS: the four slicing-by-4 tables (crc32.go:138-149's slicing8Table[0..3]) with every entry
+// stored 32 times side by side, lane j reading copy j mod 32, so a ds_read_b32 serves each 32-lane
+// group in one LDS cycle with no bank conflict (random indices into one table conflict ~3.5-way).
+// Layout (bytes): region r (tables 2r, 2r+1) at r*64 KiB, entry e at e*256 within it, table 2r+tt
+// at tt*128, copy c at c*4 -- so a lookup's address is ONE v_perm_b32 (byte 1 = the index byte,
+// byte 0 = 4c, byte 2 = r, byte 3 = 0) and the table's 128 goes in the ds_read offset.
+#ifndef EFES_SPAN_COPIES
+#define EFES_SPAN_COPIES 32
+#endif
+constexpr int kSpanCopies = EFES_SPAN_COPIES;
+#if EFES_SPAN_COPIES == 32
+constexpr int kSpanWavesPerSimd = 4;  // one workgroup per CU
 struct SpanLDS {
-  uint32_t slice[8][256][kSpanCopies];  // 128 KiB
-  uint32_t row_shift[4][256];           // 4 KiB
+  uint32_t slice[2][256][2][kSpanCopies];  // 128 KiB at LDS address 0
+  uint32_t row_shift[4][256];              // 4 KiB
   uint32_t wave_sum[kSpanLanes / 64];
 };
+#else
+// Variant: 16 copies (lanes j and j+16 of a group share one: 2-way conflicts), all four tables in
+// one 64 KiB region (entry e at e*256, table t at t*64, copy c at c*4), two workgroups per CU.
+constexpr int kSpanWavesPerSimd = 8;
+struct SpanLDS {
+  uint32_t slice[256][4][kSpanCopies];  // 64 KiB at LDS address 0
+  uint32_t row_shift[4][256];
+  uint32_t wave_sum[kSpanLanes / 64];
+};
+#endif
 
 constexpr int kLineWords = kSpanLine / 4;
+#ifndef EFES_SPAN_BUF
+#define EFES_SPAN_BUF 2
+#endif
+constexpr int kSpanBuf = EFES_SPAN_BUF;  // lines in flight per lane
 
 __device__ __forceinline__ void load_line(const uint8_t* src, uint32_t (&w)[kLineWords]) {
   typedef uint32_t v4u __attribute__((ext_vector_type(4)));
@@ -109,20 +132,35 @@ __device__ __forceinline__ void load_line(const uint8_t* src, uint32_t (&w)[kLin
   }
 }
 
-// Raw CRC (from a zero register) of one line: slicing-by-8 as crc32.go:157-161, the lookups into
-// this lane's copy of the tables.  lo / hi: &slice[0][0][c] and &slice[4][0][c] (byte addresses
-// within 16-bit ds_read offsets of their base).
-__device__ __forceinline__ uint32_t line_raw(const uint32_t* lo, const uint32_t* hi, const uint32_t (&w)[kLineWords]) {
-  constexpr int E = kSpanCopies, T = 256 * kSpanCopies;  // entry and table strides in words
-  uint32_t crc = 0;
+// v_perm_b32 selector: byte 0 <- lane byte 0 (4c), byte 1 <- x byte k, byte 2 <- lane byte 2 (r),
+// byte 3 <- 0x00 (selector 12).  Selectors 0-3 pick the second operand's bytes, 4-7 the first's.
+constexpr uint32_t perm_sel(int k) { return 0x0C020000u | ((4u + (uint32_t)k) << 8); }
+
+__device__ __forceinline__ uint32_t lds_word(const SpanLDS& L, uint32_t byte_addr, uint32_t off) {
+  return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(&L.slice) + byte_addr + off);
+}
+#if EFES_SPAN_COPIES == 32
+constexpr uint32_t kOff0 = 0, kOff1 = 128, kOff2 = 0, kOff3 = 128;  // table offsets within their region
+#else
+constexpr uint32_t kOff0 = 0, kOff1 = 64, kOff2 = 128, kOff3 = 192;
+#endif
+
+// Raw CRC (from a zero register) of one line: slicing-by-4 (the 4-byte form of crc32.go:157-161),
+// the lookups into this lane's copy.  l0 / l1: the lane's address bytes for region 0 / 1.
+__device__ __forceinline__ uint32_t line_raw(const SpanLDS& L, uint32_t l0, uint32_t l1,
+                                             const uint32_t (&w)[kLineWords]) {
+  uint32_t x = w[0], crc = 0;  // x = crc ^ the next word (crc32.go:157's crc ^= ...)
 #pragma unroll
-  for (int s = 0; s < kLineWords / 2; ++s) {
-    const uint32_t x = crc ^ w[2 * s], y = w[2 * s + 1];
-    const uint32_t a = __builtin_amdgcn_bitop3_b32(lo[0 * T + E * (y >> 24)], lo[1 * T + E * ((y >> 16) & 0xffu)],
-                                                   lo[2 * T + E * ((y >> 8) & 0xffu)], 0x96);
-    const uint32_t b = __builtin_amdgcn_bitop3_b32(lo[3 * T + E * (y & 0xffu)], hi[0 * T + E * (x >> 24)],
-                                                   hi[1 * T + E * ((x >> 16) & 0xffu)], 0x96);
-    crc = __builtin_amdgcn_bitop3_b32(a, b, hi[2 * T + E * ((x >> 8) & 0xffu)] ^ hi[3 * T + E * (x & 0xffu)], 0x96);
+  for (int s = 0; s < kLineWords; ++s) {
+    const uint32_t t0 = lds_word(L, __builtin_amdgcn_perm(x, l0, perm_sel(3)), kOff0);  // tab[0][x >> 24]
+    const uint32_t t1 = lds_word(L, __builtin_amdgcn_perm(x, l0, perm_sel(2)), kOff1);  // tab[1][x >> 16 & 0xff]
+    const uint32_t t2 = lds_word(L, __builtin_amdgcn_perm(x, l1, perm_sel(1)), kOff2);  // tab[2][x >> 8 & 0xff]
+    const uint32_t t3 = lds_word(L, __builtin_amdgcn_perm(x, l1, perm_sel(0)), kOff3);  // tab[3][x & 0xff]
+    const uint32_t p = __builtin_amdgcn_bitop3_b32(t0, t1, t2, 0x96);
+    if (s + 1 < kLineWords)
+      x = __builtin_amdgcn_bitop3_b32(p, t3, w[s + 1], 0x96);  // 6 VALU per 4 bytes
+    else
+      crc = p ^ t3;
   }
   return crc;
 }
@@ -132,13 +170,17 @@ __device__ __forceinline__ uint32_t row_advance(const uint32_t (&s)[4][256], uin
          s[3][v >> 24];
 }
 
-__global__ __launch_bounds__(kSpanLanes) void span_kernel(const SpanArgs a) {
+__global__ __launch_bounds__(kSpanLanes, kSpanWavesPerSimd) void span_kernel(const SpanArgs a) {
   __shared__ __attribute__((aligned(16))) SpanLDS L;
   {  // tables into LDS: each slicing entry kSpanCopies times (4 per ds_write_b128), the row shift once
-    const uint32_t* src = &a.tabs->slice8[0][0];
-    uint4* dst = reinterpret_cast<uint4*>(&L.slice[0][0][0]);
-    for (uint32_t i = threadIdx.x; i < 8 * 256 * kSpanCopies / 4; i += kSpanLanes) {
-      const uint32_t v = src[i / (kSpanCopies / 4)];
+    uint4* dst = reinterpret_cast<uint4*>(&L.slice);
+    for (uint32_t i = threadIdx.x; i < sizeof(L.slice) / 16; i += kSpanLanes) {
+      const uint32_t word = 4 * i;
+#if EFES_SPAN_COPIES == 32
+      const uint32_t v = a.tabs->slice8[2 * (word >> 14) + ((word >> 5) & 1u)][(word >> 6) & 255u];
+#else
+      const uint32_t v = a.tabs->slice8[(word >> 4) & 3u][word >> 6];
+#endif
       dst[i] = make_uint4(v, v, v, v);
     }
     const uint4* s2 = reinterpret_cast<const uint4*>(a.span->row_shift);
@@ -153,32 +195,44 @@ __global__ __launch_bounds__(kSpanLanes) void span_kernel(const SpanArgs a) {
   const uint32_t extra = (uint32_t)(count % kSpanLanes);  // lanes j < extra take one more line
   const uint8_t* p = a.bulk + (start + j) * kSpanLine;
   constexpr uint64_t kRow = (uint64_t)kSpanLine * kSpanLanes;
-  const uint32_t* lo = &L.slice[0][0][j % kSpanCopies];
-  const uint32_t* hi = &L.slice[4][0][j % kSpanCopies];
+#if EFES_SPAN_COPIES == 32
+  const uint32_t l0 = 4u * (j % kSpanCopies), l1 = l0 | (1u << 16);  // address bytes of regions 0 / 1
+#else
+  const uint32_t l0 = 4u * (j % kSpanCopies), l1 = l0;
+#endif
   __syncthreads();
 
   uint32_t acc = 0;
   if (rows) {
-    // two lines in flight per lane: A holds row i, B row i+1; the loads past the last row re-read
-    // the last row (clamped address, never committed)
-    uint32_t A[kLineWords], B[kLineWords];
-    load_line(p, A);
-    load_line(p + (rows > 1 ? kRow : 0), B);
-    for (uint64_t i = 0; i < rows; i += 2) {
-      const uint32_t ra = line_raw(lo, hi, A);
-      load_line(p + (i + 2 < rows ? i + 2 : rows - 1) * kRow, A);
-      acc = row_advance(L.row_shift, acc) ^ ra;
-      if (i + 1 < rows) {
-        const uint32_t rb = line_raw(lo, hi, B);
-        load_line(p + (i + 3 < rows ? i + 3 : rows - 1) * kRow, B);
-        acc = row_advance(L.row_shift, acc) ^ rb;
+    // kSpanBuf lines in flight per lane: buffer k holds row g*kSpanBuf + k.  The loop body is
+    // branch-free so the compiler's vmcnt waits stay exact (a conditional load made it wait for
+    // every line): reloads past the last row re-read the last row (clamped address, never
+    // committed), and the rows % kSpanBuf left over are already in buffers 0.. after the loop.
+    // Scheduling barriers keep "chain of buffer k, reload buffer k" in order: left to itself the
+    // compiler interleaves the chains and waits for all lines before issuing any reload.
+    uint32_t buf[kSpanBuf][kLineWords];
+    const uint64_t groups_of_rows = rows / kSpanBuf, last = rows - 1;
+#pragma unroll
+    for (int k = 0; k < kSpanBuf; ++k) load_line(p + ((uint64_t)k < last ? k : last) * kRow, buf[k]);
+    for (uint64_t g = 0; g < groups_of_rows; ++g) {
+#pragma unroll
+      for (int k = 0; k < kSpanBuf; ++k) {
+        const uint32_t rk = line_raw(L, l0, l1, buf[k]);
+        __builtin_amdgcn_sched_barrier(0);
+        const uint64_t nxt = (g + 1) * kSpanBuf + k;
+        load_line(p + (nxt < last ? nxt : last) * kRow, buf[k]);
+        __builtin_amdgcn_sched_barrier(0);
+        acc = row_advance(L.row_shift, acc) ^ rk;
       }
     }
+#pragma unroll
+    for (int k = 0; k < kSpanBuf - 1; ++k)
+      if ((uint64_t)k < rows % kSpanBuf) acc = row_advance(L.row_shift, acc) ^ line_raw(L, l0, l1, buf[k]);
   }
   if (j < extra) {  // the partial last row
     uint32_t E[kLineWords];
     load_line(p + rows * kRow, E);
-    acc = row_advance(L.row_shift, acc) ^ line_raw(lo, hi, E);
+    acc = row_advance(L.row_shift, acc) ^ line_raw(L, l0, l1, E);
   }
   // Lane j's last line is followed, within the range, by (extra - 1 - j) mod L lines.
   const uint32_t after = (extra + kSpanLanes - 1 - j) % kSpanLanes;
@@ -207,11 +261,17 @@ hipError_t launch_crc_span(const void* data, uint64_t length, uint32_t* crc, con
                      bulk + nline * kSpanLine, xpow8n(m), crc, tabs);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || nline == 0) return e;
-  // Workgroups: one per CU (132 KiB of LDS tables, 16 waves), at least 4 rows per lane.
+  // Workgroups: as many as are resident at once (kSpanWavesPerSimd / 4 per CU), at least 4 rows
+  // per lane.
   uint64_t groups = (nline + 4ull * kSpanLanes - 1) / (4ull * kSpanLanes);
-  const uint64_t cap = (uint64_t)(cus > 0 ? cus : 256) < kSpanMaxGroups ? (uint64_t)(cus > 0 ? cus : 256)
-                                                                      : (uint64_t)kSpanMaxGroups;
+  const uint64_t per_cu = kSpanWavesPerSimd / 4, resident = (uint64_t)(cus > 0 ? cus : 256) * per_cu;
+  const uint64_t cap = resident < kSpanMaxGroups ? resident : (uint64_t)kSpanMaxGroups;
   if (groups > cap) groups = cap;
+  if (const char* e = getenv("EFES_SPAN_GROUPS")) {  // developer override for calibration
+    const uint64_t g = strtoull(e, nullptr, 10);
+    if (g >= 1 && g <= kSpanMaxGroups) groups = g;
+  }
+  if (groups > nline) groups = nline;
   if (groups == 0) groups = 1;
   SpanArgs a{};
   a.bulk = bulk;

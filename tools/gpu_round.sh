@@ -24,11 +24,11 @@ for s in $STEPS; do
     bench_*) a=${s#bench_}; timeout -k 10 400 python bench.py --no-cpu-baseline --mode ${a} > $OUT/bench_${TAG}_$a.json 2> $OUT/bench_${TAG}_$a.err; rc=$?
            echo "$s rc=$rc"; cat $OUT/bench_${TAG}_$a.json; fatal $rc $OUT/bench_${TAG}_$a.err ;;
     prof)  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o run -- \
-               python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --host-inclusive off --ingest-leg off --mixed-leg off --concurrency-leg off --uploads-leg off > $OUT/prof_$TAG.log 2>&1; rc=$?
+               python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --host-inclusive off --ingest-leg off --mixed-leg off --concurrency-leg off --uploads-leg off --receiver-leg off --span-leg off > $OUT/prof_$TAG.log 2>&1; rc=$?
            echo "prof rc=$rc"; tail -3 $OUT/prof_$TAG.log; fatal $rc $OUT/prof_$TAG.log
            find $OUT/prof_$TAG -name "*kernel_stats.csv" -exec cat {} \; ;;
     pmc)   timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_$TAG -o run -- \
-               python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --host-inclusive off --ingest-leg off --mixed-leg off --concurrency-leg off --uploads-leg off > $OUT/pmc_$TAG.log 2>&1; rc=$?
+               python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --host-inclusive off --ingest-leg off --mixed-leg off --concurrency-leg off --uploads-leg off --receiver-leg off --span-leg off > $OUT/pmc_$TAG.log 2>&1; rc=$?
            echo "pmc rc=$rc"; tail -3 $OUT/pmc_$TAG.log; fatal $rc $OUT/pmc_$TAG.log
            find $OUT/pmc_$TAG -name "*.csv" | head ;;
     *) echo "unknown step $s"; exit 2 ;;

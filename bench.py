@@ -89,7 +89,7 @@ def parse_args(argv=None):
                         "flight, 8192 x 4 MiB, 32 KiB pageable Writes, Sum each); auto = N=1 only")
     p.add_argument("--receiver-leg", choices=["auto", "on", "off"], default="auto",
                    help="also report the receiver with files (tools/bench_receiver: saveFile through ServeHTTP, "
-                        "512 request threads x 4 MiB PATCHes on tmpfs) and Sha1File read-back (256 threads); auto = N=1 only")
+                        "768 request threads x 4 MiB PATCHes on tmpfs) and Sha1File read-back (256 threads); auto = N=1 only")
     p.add_argument("--concurrency-leg", choices=["auto", "on", "off"], default="auto",
                    help="also report 4 MiB chunks at 1K..192K in flight, one AUTO launch each (auto = N=1 only)")
     p.add_argument("--mixed-leg", choices=["auto", "on", "off"], default="auto",
@@ -255,11 +255,11 @@ def receiver_leg():
     base = "/dev/shm" if os.access("/dev/shm", os.W_OK) else tempfile.gettempdir()
     out = {}
     with tempfile.TemporaryDirectory(dir=base, prefix="efes_receiver_") as d:
-        # 512 request threads: the GPU box counts threads against a 1024-process limit, and 1024 of
-        # them beside this process's own runtime threads crossed it (12.0-14.9 GiB/s at 1024
-        # threads, 13.1 at 512: DESIGN.md "The receiver with files")
-        for key, argv, size in (("receiver", ["receiver", d, "512", "4", str(4 << 20), str(4 << 20)], 4 << 20),
-                                ("copy", ["copy", d, "512", "4", str(4 << 20)], 0),
+        # 768 request threads: the GPU box counts threads against a 1024-process limit, and 1024 of
+        # them beside this process's own runtime threads crossed it once (under rocprof); 768
+        # leaves ~200 for the runtimes (12.0-19.0 GiB/s at 1024 threads, 12.7-13.1 at 512)
+        for key, argv, size in (("receiver", ["receiver", d, "768", "4", str(4 << 20), str(4 << 20)], 4 << 20),
+                                ("copy", ["copy", d, "768", "4", str(4 << 20)], 0),
                                 ("sha1file", ["sha1file", d, "256", "4", str(4 << 20)], 4 << 20)):
             r = subprocess.run([exe] + argv, check=True, capture_output=True, text=True, timeout=300)
             res = json.loads(r.stdout.strip().splitlines()[-1])

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define EFES_ABI_VERSION 3
+#define EFES_ABI_VERSION 4
 
 /* ---- error codes ---------------------------------------------------------------- */
 #define EFES_OK 0

@@ -8,7 +8,7 @@ cd "$(dirname "$0")/.."
 mkdir -p efes_amd/lib/tsan
 HIPCC=${HIPCC:-/opt/rocm/bin/hipcc}
 $HIPCC --offload-arch=gfx950 -O1 -g -std=c++17 -fPIC -shared -Xarch_host -fsanitize=thread -I include \
-  -o efes_amd/lib/tsan/libefeshash.so efes_amd/csrc/efes_kernels.hip efes_amd/csrc/efes_api.cpp \
+  -o efes_amd/lib/tsan/libefeshash.so efes_amd/csrc/efes_kernels.hip efes_amd/csrc/efes_crc_span.hip efes_amd/csrc/efes_api.cpp \
   efes_amd/csrc/efes_ingest.cpp efes_amd/csrc/efes_queue.cpp efes_amd/csrc/efes_stream.cpp efes_amd/csrc/efes_plan.cpp
 $HIPCC -O1 -g -std=c++17 -fsanitize=thread -I include tools/bench_uploads.cpp -o tools/bench_uploads_tsan \
   -L efes_amd/lib/tsan -lefeshash -Wl,-rpath,'$ORIGIN/../efes_amd/lib/tsan' -pthread

@@ -108,3 +108,26 @@ def test_span_zero_bytes_and_constant_data(env):
         buf = torch.full((n,), v, dtype=torch.uint8, device="cuda:0")
         assert _span(env, buf, 0, n) == zlib.crc32(bytes([v]) * n)
         assert _span(env, buf, 1, n - 1, 0x12345678) == zlib.crc32(bytes([v]) * (n - 1), 0x12345678)
+
+
+def test_span_concurrent_streams_and_null(env):
+    """Calls on different streams at once keep their states apart (no shared scratch: every
+    workgroup XORs into its own call's state); length 0 with a NULL pointer leaves the state."""
+    torch = env["torch"]
+    n = (64 << 20) + 77
+    bufs = [_device_bytes(env, n, 100 + i) for i in range(4)]
+    expect = [zlib.crc32(b.cpu().numpy(), 7 * i) for i, b in enumerate(bufs)]
+    streams = [torch.cuda.Stream(device="cuda:0") for _ in bufs]
+    states = [torch.tensor([7 * i], dtype=torch.int64, device="cuda:0") for i in range(len(bufs))]
+    torch.cuda.synchronize()
+    for rep in range(3):
+        for i, (b, s, st) in enumerate(zip(bufs, streams, states)):
+            with torch.cuda.stream(s):
+                st.fill_(7 * i)
+                env["ctx"].crc32_span(b.data_ptr(), n, st.data_ptr(), s.cuda_stream)
+        torch.cuda.synchronize()
+        assert [int(st.item()) & 0xFFFFFFFF for st in states] == expect, rep
+    st = torch.tensor([0xCAFEF00D], dtype=torch.int64, device="cuda:0")
+    env["ctx"].crc32_span(0, 0, st.data_ptr(), None)
+    env["ctx"].sync()
+    assert int(st.item()) == 0xCAFEF00D

@@ -128,6 +128,7 @@ def test_span_concurrent_streams_and_null(env):
         torch.cuda.synchronize()
         assert [int(st.item()) & 0xFFFFFFFF for st in states] == expect, rep
     st = torch.tensor([0xCAFEF00D], dtype=torch.int64, device="cuda:0")
+    torch.cuda.synchronize()  # the call below runs on the context's own (non-blocking) stream
     env["ctx"].crc32_span(0, 0, st.data_ptr(), None)
     env["ctx"].sync()
     assert int(st.item()) == 0xCAFEF00D

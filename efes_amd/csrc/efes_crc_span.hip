@@ -94,27 +94,15 @@ __global__ __launch_bounds__(64) void span_prep_kernel(const uint8_t* __restrict
 // Layout (bytes): region r (tables 2r, 2r+1) at r*64 KiB, entry e at e*256 within it, table 2r+tt
 // at tt*128, copy c at c*4 -- so a lookup's address is ONE v_perm_b32 (byte 1 = the index byte,
 // byte 0 = 4c, byte 2 = r, byte 3 = 0) and the table's 128 goes in the ds_read offset.
-#ifndef EFES_SPAN_COPIES
-#define EFES_SPAN_COPIES 32
-#endif
-constexpr int kSpanCopies = EFES_SPAN_COPIES;
-#if EFES_SPAN_COPIES == 32
+// (Measured and not kept: 16 copies in one 64 KiB region with two workgroups per CU -- 2-way
+// conflicts, 32 waves per CU -- ran at the same rate; DESIGN.md §4 "Span CRC".)
+constexpr int kSpanCopies = 32;
 constexpr int kSpanWavesPerSimd = 4;  // one workgroup per CU
 struct SpanLDS {
   uint32_t slice[2][256][2][kSpanCopies];  // 128 KiB at LDS address 0
   uint32_t row_shift[4][256];              // 4 KiB
   uint32_t wave_sum[kSpanLanes / 64];
 };
-#else
-// Variant: 16 copies (lanes j and j+16 of a group share one: 2-way conflicts), all four tables in
-// one 64 KiB region (entry e at e*256, table t at t*64, copy c at c*4), two workgroups per CU.
-constexpr int kSpanWavesPerSimd = 8;
-struct SpanLDS {
-  uint32_t slice[256][4][kSpanCopies];  // 64 KiB at LDS address 0
-  uint32_t row_shift[4][256];
-  uint32_t wave_sum[kSpanLanes / 64];
-};
-#endif
 
 constexpr int kLineWords = kSpanLine / 4;
 #ifndef EFES_SPAN_BUF
@@ -139,11 +127,7 @@ constexpr uint32_t perm_sel(int k) { return 0x0C020000u | ((4u + (uint32_t)k) <<
 __device__ __forceinline__ uint32_t lds_word(const SpanLDS& L, uint32_t byte_addr, uint32_t off) {
   return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(&L.slice) + byte_addr + off);
 }
-#if EFES_SPAN_COPIES == 32
 constexpr uint32_t kOff0 = 0, kOff1 = 128, kOff2 = 0, kOff3 = 128;  // table offsets within their region
-#else
-constexpr uint32_t kOff0 = 0, kOff1 = 64, kOff2 = 128, kOff3 = 192;
-#endif
 
 // Raw CRC (from a zero register) of one line: slicing-by-4 (the 4-byte form of crc32.go:157-161),
 // the lookups into this lane's copy.  l0 / l1: the lane's address bytes for region 0 / 1.
@@ -175,12 +159,8 @@ __global__ __launch_bounds__(kSpanLanes, kSpanWavesPerSimd) void span_kernel(con
   {  // tables into LDS: each slicing entry kSpanCopies times (4 per ds_write_b128), the row shift once
     uint4* dst = reinterpret_cast<uint4*>(&L.slice);
     for (uint32_t i = threadIdx.x; i < sizeof(L.slice) / 16; i += kSpanLanes) {
-      const uint32_t word = 4 * i;
-#if EFES_SPAN_COPIES == 32
+      const uint32_t word = 4 * i;  // region word >> 14, entry (word >> 6) & 255, table pair bit 5
       const uint32_t v = a.tabs->slice8[2 * (word >> 14) + ((word >> 5) & 1u)][(word >> 6) & 255u];
-#else
-      const uint32_t v = a.tabs->slice8[(word >> 4) & 3u][word >> 6];
-#endif
       dst[i] = make_uint4(v, v, v, v);
     }
     const uint4* s2 = reinterpret_cast<const uint4*>(a.span->row_shift);
@@ -195,11 +175,7 @@ __global__ __launch_bounds__(kSpanLanes, kSpanWavesPerSimd) void span_kernel(con
   const uint32_t extra = (uint32_t)(count % kSpanLanes);  // lanes j < extra take one more line
   const uint8_t* p = a.bulk + (start + j) * kSpanLine;
   constexpr uint64_t kRow = (uint64_t)kSpanLine * kSpanLanes;
-#if EFES_SPAN_COPIES == 32
   const uint32_t l0 = 4u * (j % kSpanCopies), l1 = l0 | (1u << 16);  // address bytes of regions 0 / 1
-#else
-  const uint32_t l0 = 4u * (j % kSpanCopies), l1 = l0;
-#endif
   __syncthreads();
 
   uint32_t acc = 0;

@@ -132,3 +132,26 @@ def test_span_concurrent_streams_and_null(env):
     env["ctx"].crc32_span(0, 0, st.data_ptr(), None)
     env["ctx"].sync()
     assert int(st.item()) == 0xCAFEF00D
+
+
+def test_span_pieces_on_two_contexts_combine(env):
+    """One object over two contexts (standing in for two GPUs, efes_amd/shard.py): each spans its
+    piece from a zero state, the 4-byte results fold in piece order == one call == zlib."""
+    from efes_amd.hashing import Context
+    from efes_amd.shard import combine_piece_crcs, piece_bounds
+    torch = env["torch"]
+    n = (96 << 20) + 4097
+    buf = _device_bytes(env, n, 0xAB)
+    ctxs = [env["ctx"], Context(0)]
+    try:
+        pieces = []
+        for ctx, (a, m) in zip(ctxs, piece_bounds(n, 2)):
+            st = torch.zeros(1, dtype=torch.int64, device="cuda:0")
+            torch.cuda.synchronize()
+            ctx.crc32_span(buf.data_ptr() + a, m, st.data_ptr(), None)
+            ctx.sync()
+            pieces.append((int(st.item()) & 0xFFFFFFFF, m))
+        whole = _span(env, buf, 0, n)
+        assert combine_piece_crcs(pieces) == whole == zlib.crc32(buf.cpu().numpy())
+    finally:
+        ctxs[1].close()

@@ -9,19 +9,19 @@
 // (the crc32_combine identity, efes_crc32_combine in efes_api.cpp), and Go's finalized update is
 // crc' = ~(Z^n(~crc) ^ raw(p)) (crc32.go:123,127).
 //
-// Layout of one launch over n = head + 128*nline + rest bytes:
+// Layout of one launch over n = head + 64*nline + rest bytes (kSpanLine = 64):
 //   * span_prep_kernel (one lane): the <= 15 head bytes up to the first 16-byte boundary and the
-//     < 128 rest bytes byte-wise (crc32.go:125); the state becomes ~Z^m(~crc_head) ^ raw(rest)
+//     < 64 rest bytes byte-wise (crc32.go:125); the state becomes ~Z^m(~crc_head) ^ raw(rest)
 //     with m the bytes after the head -- every bulk contribution below is then XORed into it;
-//   * span_kernel: workgroup w owns a contiguous range of 128-byte lines; lane j takes lines j,
-//     j+L, j+2L, ... (a wave reads 8 KiB per row), computes each line's raw CRC by slicing-by-4
+//   * span_kernel: workgroup w owns a contiguous range of 64-byte lines; lane j takes lines j,
+//     j+L, j+2L, ... (a wave reads 4 KiB per row), computes each line's raw CRC by slicing-by-4
 //     from lane-private copies of the tables in LDS (no bank conflicts, one v_perm per lookup
-//     address) and folds it into its accumulator, acc = Z^(128L)(acc) ^ raw(line) (a byte-sliced
+//     address) and folds it into its accumulator, acc = Z^(64L)(acc) ^ raw(line) (a byte-sliced
 //     4 x 256 table).  At the end, lane j's accumulator is advanced over the lines of the range
-//     after its last line (one GF(2) product with lane_op[k] = x^(8*128*k)), the lanes are
+//     after its last line (one GF(2) product with lane_op[k] = x^(8*64*k)), the lanes are
 //     XOR-reduced, the sum is advanced over the bytes after the range (op[w], computed on the
 //     host) and XORed into the state with one atomic per workgroup.
-// Bound: HBM read (every byte once); measured at ~85 % of a pure read kernel (DESIGN.md §4 "Span
+// Bound: HBM read (every byte once); measured at ~93 % of a pure read kernel (DESIGN.md §4 "Span
 // CRC").  No SHA-1, no MFMA.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -98,6 +98,7 @@ __global__ __launch_bounds__(64) void span_prep_kernel(const uint8_t* __restrict
 // conflicts, 32 waves per CU -- ran at the same rate; DESIGN.md §4 "Span CRC".)
 constexpr int kSpanCopies = 32;
 constexpr int kSpanWavesPerSimd = 4;  // one workgroup per CU
+// (The row shift keeps one copy: 2 or 4 copies measured no faster, DESIGN.md.)
 struct SpanLDS {
   uint32_t slice[2][256][2][kSpanCopies];  // 128 KiB at LDS address 0
   uint32_t row_shift[4][256];              // 4 KiB
@@ -115,7 +116,11 @@ __device__ __forceinline__ void load_line(const uint8_t* src, uint32_t (&w)[kLin
   const __attribute__((address_space(1))) v4u* s = (const __attribute__((address_space(1))) v4u*)src;
 #pragma unroll
   for (int q = 0; q < kLineWords / 4; ++q) {
+#ifdef EFES_SPAN_NT
+    const v4u v = __builtin_nontemporal_load(s + q);  // A/B knob: read once, nt policy
+#else
     const v4u v = s[q];
+#endif
     w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
   }
 }

@@ -60,11 +60,14 @@ hipError_t launch_fed(const efes_job* jobs, uint32_t njobs, const Tables* tabs, 
 hipError_t launch_fill(void* dst, size_t bytes, uint64_t seed, hipStream_t s);
 
 // Span CRC (efes_crc_span.hip): CRC-32 of one long buffer on the whole GPU.  Bytes per lane per
-// row (one 128-B cache line), lanes per workgroup, the workgroup cap (the host passes each
+// row (64: half a 128-B cache line, measured fastest), lanes per workgroup, the workgroup cap (the host passes each
 // workgroup's combine operator as a kernel argument), and the per-context operator tables:
 // row_shift advances a raw register over one workgroup row (kSpanLanes lines), byte-sliced;
 // lane_op[k] = x^(8*kSpanLine*k) mod P.
-constexpr int kSpanLine = 128;
+#ifndef EFES_SPAN_LINE
+#define EFES_SPAN_LINE 64
+#endif
+constexpr int kSpanLine = EFES_SPAN_LINE;  // bytes per lane per row (A/B: 16, 32, 48, 64, 128)
 constexpr int kSpanLanes = 1024;
 constexpr int kSpanMaxGroups = 512;
 struct SpanTables {

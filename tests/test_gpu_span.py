@@ -42,12 +42,12 @@ def _device_bytes(env, nbytes: int, seed: int):
     return buf
 
 
-# lengths around every boundary of the decomposition: the 16-byte head, the < 128-byte rest,
-# 128-byte lines, one workgroup row (1024 lines = 128 KiB), partial and whole rows, several rows
-# per lane, ragged workgroup ranges
-LENGTHS = [0, 1, 15, 16, 17, 63, 64, 65, 127, 128, 129, 143, 144, 1000, 4095, 4096, 4097, 32768 + 5,
-           131071, 131072, 131073, 131072 + 128 * 7 + 5, 262144 + 3, 524288 + 127, (1 << 20) + 13,
-           3 * (1 << 20) - 1]
+# lengths around every boundary of the decomposition: the 16-byte head, the < 64-byte rest,
+# 64-byte lines, one workgroup row (1024 lines = 64 KiB), partial and whole rows, several rows
+# per lane, ragged workgroup ranges (and the 128-byte / 128 KiB edges of other line sizes)
+LENGTHS = [0, 1, 15, 16, 17, 63, 64, 65, 79, 80, 81, 127, 128, 129, 143, 144, 1000, 4095, 4096, 4097,
+           32768 + 5, 65535, 65536, 65537, 65536 + 64 * 7 + 5, 131071, 131072, 131073, 131072 + 128 * 7 + 5,
+           262144 + 3, 524288 + 127, (1 << 20) + 13, 3 * (1 << 20) - 1]
 
 
 def test_span_matches_oracle_small(env):

@@ -83,13 +83,19 @@ def parse_args(argv=None):
                    help="also time the host-resident path (pinned H2D + hash); auto = N=1 only")
     p.add_argument("--segment-bytes", type=int, default=256 << 10, help="host-inclusive pipeline segment")
     p.add_argument("--ingest-leg", choices=["auto", "on", "off"], default="auto",
-                   help="also report BASELINE configs[4] per-GPU (auto = N=1 only)")
+                   help="also report BASELINE configs[4]: each GPU's share of 10 TiB, aggregated over all ranks "
+                        "(auto = on at every N)")
+    p.add_argument("--sha1-leg", choices=["auto", "on", "off"], default="auto",
+                   help="also report BASELINE configs[1] (the same chunks, SHA-1 only); auto = N=1 only")
     p.add_argument("--uploads-leg", choices=["auto", "on", "off"], default="auto",
                    help="also report the server path (tools/bench_uploads: 32 request threads x 256 uploads in "
                         "flight, 8192 x 4 MiB, 32 KiB pageable Writes, Sum each); auto = N=1 only")
     p.add_argument("--receiver-leg", choices=["auto", "on", "off"], default="auto",
                    help="also report the receiver with files (tools/bench_receiver: saveFile through ServeHTTP, "
                         "768 request threads x 4 MiB PATCHes on tmpfs) and Sha1File read-back (256 threads); auto = N=1 only")
+    p.add_argument("--drain-leg", choices=["auto", "on", "off"], default="auto",
+                   help="also report the drainer's read-back (sendFile/Sha1File mirror, K files in flight) against "
+                        "the CPU port; auto = N=1 only")
     p.add_argument("--concurrency-leg", choices=["auto", "on", "off"], default="auto",
                    help="also report 4 MiB chunks at 1K..192K in flight, one AUTO launch each (auto = N=1 only)")
     p.add_argument("--mixed-leg", choices=["auto", "on", "off"], default="auto",
@@ -251,30 +257,106 @@ def receiver_leg():
     import tempfile
     import zlib
 
+    import statistics
+
     exe = os.path.join(ROOT, "tools", "bench_receiver")
     base = "/dev/shm" if os.access("/dev/shm", os.W_OK) else tempfile.gettempdir()
     out = {}
+
+    def run(argv, env=None):
+        r = subprocess.run([exe] + argv, check=True, capture_output=True, text=True, timeout=300,
+                           env=dict(os.environ, **(env or {})))
+        return json.loads(r.stdout.strip().splitlines()[-1])
+
+    src = _xorshift_bytes(4 << 20)
     with tempfile.TemporaryDirectory(dir=base, prefix="efes_receiver_") as d:
         # 768 request threads: the GPU box counts threads against a 1024-process limit, and 1024 of
         # them beside this process's own runtime threads crossed it once (under rocprof); 768
-        # leaves ~200 for the runtimes (12.0-19.0 GiB/s at 1024 threads, 12.7-13.1 at 512)
-        for key, argv, size in (("receiver", ["receiver", d, "768", "4", str(4 << 20), str(4 << 20)], 4 << 20),
-                                ("copy", ["copy", d, "768", "4", str(4 << 20)], 0),
-                                ("sha1file", ["sha1file", d, "256", "4", str(4 << 20)], 4 << 20)):
-            r = subprocess.run([exe] + argv, check=True, capture_output=True, text=True, timeout=300)
-            res = json.loads(r.stdout.strip().splitlines()[-1])
-            if key == "copy":  # the same io.Copy without the digests: the host's ceiling for `receiver`
-                out["receiver"]["copy_ceiling"] = res["value"]
-                out["receiver"]["frac_of_copy"] = round(out["receiver"]["value"] / res["value"], 3)
-                continue
-            src = _xorshift_bytes(size)
-            want = hashlib.sha1(src).hexdigest() + ("%08x" % zlib.crc32(src) if key == "receiver" else "")
-            got = res.pop("sum_sha1_crc32" if key == "receiver" else "sum_sha1")
-            res["digests_match"] = got == want and res.pop("all_sums_equal")
-            out[key] = res
-    out["note"] = ("receiver: saveFile with the digests on the GPU; copy_ceiling: the same requests' io.Copy "
-                   "(32 KiB reads, write, fsync) with no hashing at all, on the same host cores; not `value`")
+        # leaves ~200 for the runtimes (12.0-19.0 GiB/s at 1024 threads, 12.7-13.1 at 512).
+        # Receiver and copy ceiling alternate, three times: the fraction is the median of the pairs.
+        recv, copy, fracs, ok = [], [], [], True
+        want = hashlib.sha1(src).hexdigest() + "%08x" % zlib.crc32(src)
+        for _ in range(3):
+            r = run(["receiver", d, "768", "4", str(4 << 20), str(4 << 20)])
+            ok = ok and r.pop("sum_sha1_crc32") == want and r.pop("all_sums_equal")
+            c = run(["copy", d, "768", "4", str(4 << 20)])
+            recv.append(r)
+            copy.append(c["value"])
+            fracs.append(r["value"] / c["value"])
+        res = dict(recv[0])
+        res.update({"value": round(statistics.median(x["value"] for x in recv), 3),
+                    "values": [x["value"] for x in recv], "copy_ceiling": round(statistics.median(copy), 3),
+                    "copy_values": copy, "frac_of_copy": round(statistics.median(fracs), 3),
+                    "frac_of_copy_each": [round(f, 3) for f in fracs], "digests_match": bool(ok)})
+        # one more receiver run with saveFile's host-time accounting by phase (efes_receiver.cpp)
+        ph = run(["receiver", d, "768", "4", str(4 << 20), str(4 << 20)], {"EFES_RECEIVER_PHASES": "1"})
+        res["phases"] = {"value": ph["value"], "share_of_thread_time": ph.get("phase_share_of_thread_time")}
+        out["receiver"] = res
+        r = run(["sha1file", d, "256", "4", str(4 << 20)])
+        r["digests_match"] = r.pop("sum_sha1") == hashlib.sha1(src).hexdigest() and r.pop("all_sums_equal")
+        out["sha1file"] = r
+    out["note"] = ("receiver: saveFile with the digests on the GPU (median of 3); copy_ceiling: the same PATCHes "
+                   "without the digests -- createFile with its .info, io.Copy in 32 KiB reads, fsync, close, "
+                   "DeleteFileInfo -- on the same host cores; not `value`")
     return out
+
+
+def drain_leg(workers=(1, 16, 64, 256, 512), file_bytes: int = 4 << 20, cpu_threads: int = 16):
+    """The drainer's read-back (drain.go:87-125 -> write.go:68-117 sendFile ->
+    sha1file.go): files on tmpfs moved by K concurrent workers through the C++ sendFile/Sha1File
+    mirror, every read hashed on the GPU (their streams batched by the digest queue), to a sink
+    server; against the CPU port -- the oracle's sha1digest over the same files in 32 KiB reads on
+    `cpu_threads` host threads.  Reports the K at which the GPU path overtakes the CPU."""
+    import concurrent.futures
+    import hashlib
+    import subprocess
+    import tempfile
+
+    from oracle import oracle
+
+    exe = os.path.join(ROOT, "tools", "bench_receiver")
+    base = "/dev/shm" if os.access("/dev/shm", os.W_OK) else tempfile.gettempdir()
+    src = _xorshift_bytes(file_bytes)
+    want = hashlib.sha1(src).hexdigest()
+    nfiles = 256
+    points = []
+    with tempfile.TemporaryDirectory(dir=base, prefix="efes_drain_") as d:
+        for i in range(nfiles):
+            with open(os.path.join(d, f"{i}.fid"), "wb") as f:
+                f.write(src)
+        for k in workers:
+            fids = max(8, 4 * k)
+            r = subprocess.run([exe, "drain", d, str(k), str(fids), str(file_bytes), str(nfiles)], check=True,
+                               capture_output=True, text=True, timeout=300)
+            res = json.loads(r.stdout.strip().splitlines()[-1])
+            points.append({"workers": k, "fids": fids, "GiB/s": res["value"],
+                           "digests_match": res["sum_sha1"] == want and res["all_sums_equal"] and not res["errors"]})
+
+        def cpu_one(i):  # Sha1File's hashing (sha1file.go:23-37) on the CPU port: 32 KiB reads, one Write each
+            h = oracle.Sha1()
+            with open(os.path.join(d, f"{i % nfiles}.fid"), "rb", buffering=0) as f:
+                while True:
+                    b = f.read(32 << 10)
+                    if not b:
+                        break
+                    h.write(b)
+            return h.hexdigest() == want
+
+        oracle.build()
+        n_cpu, t0 = 0, time.perf_counter()
+        ok_cpu = True
+        with concurrent.futures.ThreadPoolExecutor(cpu_threads) as ex:
+            while time.perf_counter() - t0 < 3.0:
+                ok_cpu = all(ex.map(cpu_one, range(n_cpu, n_cpu + 4 * cpu_threads))) and ok_cpu
+                n_cpu += 4 * cpu_threads
+        cpu = n_cpu * file_bytes / (time.perf_counter() - t0) / GiB
+    over = next((p["workers"] for p in points if p["GiB/s"] > cpu), None)
+    return {"unit": "GiB/s", "file_bytes": file_bytes, "points": points,
+            "cpu_port": {"value": round(cpu, 3), "cores": cpu_threads, "kind": "port", "digests_match": bool(ok_cpu),
+                         "sample": f"{n_cpu} x {file_bytes >> 20} MiB files, oracle sha1digest in 32 KiB reads"},
+            "gpu_overtakes_cpu_at_workers": over,
+            "note": "sendFile(Sha1File) per file to a sink server (its SHA-1 answer known), K files in flight; "
+                    "one stream is one SHA-1 chain (~90 MB/s), so the GPU needs many files in flight; not `value`"}
 
 
 def make_workload(args, rank: int, world: int, ctx, device: str, stream):
@@ -396,9 +478,12 @@ def run_timed(batches, steps: int, warmup: int, mode: int, device: str, stream, 
     return wall, ev0.elapsed_time(ev1) / max(1, steps)
 
 
-def ingest_leg(args, rank: int, world: int, ctx, device: str, stream, mode: int):
+def ingest_leg(args, rank: int, world: int, ctx, device: str, stream, mode: int, dist=None):
     """BASELINE configs[4] beside the metric: this GPU's share of a 10 TiB ingest of 4 MiB
-    chunks (327 680 chunks, per-GPU queue) in launches of 131 072 chunks aliasing a 64 GiB pool."""
+    chunks (327 680 chunks, per-GPU queue) in launches of 196 608 chunks aliasing a 64 GiB pool.
+    At N > 1 every rank hashes its own share (weak scaling, no data-path collective): the launches
+    are bracketed by a barrier + synchronize on every rank, the wall time is the max over ranks and
+    the value is the bytes of ALL ranks over it (the north_star's 10 TiB over 8 GPUs at N = 8)."""
     import argparse as _ap
 
     import torch
@@ -410,19 +495,55 @@ def ingest_leg(args, rank: int, world: int, ctx, device: str, stream, mode: int)
     a.workload, a.ingest_batch, a.ingest_scale = "ingest", 196608, args.ingest_scale
     with torch.cuda.stream(stream):
         data, batches, step_bytes, config = make_workload(a, rank, world, ctx, device, stream)
-        wall, kernel_ms = run_timed(batches, len(batches), 1, mode, device, stream, None)
+        wall, kernel_ms = run_timed(batches, len(batches), 1, mode, device, stream, dist)
+    from efes_amd.shard import max_over_ranks
+
+    wall = max_over_ranks(wall, device if args.dist_backend == "nccl" else None)
     total = sum(step_bytes)
     per_launch = total / len(batches)
     achieved = per_launch / (kernel_ms * 1e-3) / 1e9
     per_launch_jobs = batches[0].n
     del data, batches
     torch.cuda.empty_cache()
-    return {"value": round(total / wall / GiB, 3), "unit": "GiB/s", "workload": config["workload"],
+    return {"value": round(world * total / wall / GiB, 3), "unit": "GiB/s", "n_gpus": world,
+            "scaling": "weak", "bytes_per_gpu": total, "max_rank_wall_s": round(wall, 4),
+            "workload": config["workload"],
             "chunks": config["chunks_per_gpu"], "launches": config["launches"], "kernel": "wide_kernel",
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 5), "kernel_ms": round(kernel_ms, 3)},
             "binding_roofline": binding_roofline("wide_kernel", achieved, per_launch_jobs, args.sha1_only),
-            "note": "many concurrent chunks per GPU (configs[4] per-GPU queue); not `value`"}
+            "note": "many concurrent chunks per GPU (configs[4] per-GPU queue); value = all ranks' bytes / the "
+                    "slowest rank's wall time; roofline = this rank's kernel; not the headline `value`"}
+
+
+def sha1_only_leg(args, ctx, data, fused, device: str, stream):
+    """BASELINE configs[1] beside the metric: the same 1024 x 4 MiB device-resident chunks, SHA-1
+    only (jobs without a CRC-32 state, sha1.go alone), K timed launches like the headline, with
+    its own roofline; digests checked against the fused run's."""
+    import numpy as np
+    import torch
+
+    from efes_amd import MODE_AUTO
+    from efes_amd._lib import lib
+    from efes_amd.batch import DeviceBatch
+
+    n, chunk = args.chunks, args.chunk_bytes
+    with torch.cuda.stream(stream):
+        b = DeviceBatch(data.data_ptr(), np.arange(n, dtype=np.uint64) * chunk, np.full(n, chunk), crc32=False,
+                        fresh=True, ctx=ctx, device=device)
+        wall, kernel_ms = run_timed([b], args.steps, 1, MODE_AUTO, device, stream, None)
+    kernel = kernel_names()[lib().efes_auto_mode(ctx.handle, n)]
+    achieved = n * chunk / (kernel_ms * 1e-3) / 1e9
+    ok = b.sha1_hex() == fused.sha1_hex() and bool((b.sums_host()[:, 20:] == 0).all())
+    return {"value": round(args.steps * n * chunk / wall / GiB, 3), "unit": "GiB/s",
+            "workload": f"{n} x {chunk >> 20} MiB chunks, SHA-1 only (BASELINE configs[1])", "kernel": kernel,
+            "steps": args.steps, "ms_per_step": round(wall * 1e3 / args.steps, 4),
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBPS, 5), "kernel_ms": round(kernel_ms, 4),
+                         "traffic": load_traffic(kernel, f"{n}x{chunk}:sha1")},
+            "binding_roofline": binding_roofline(kernel, achieved, n, True) if kernel in ("deep_kernel", "wide_kernel")
+            else None,
+            "digests_match_fused_sha1": ok, "note": "same chunks as the metric, SHA-1 only; not `value`"}
 
 
 def concurrency_leg(args, ctx, device: str, stream):
@@ -635,14 +756,18 @@ def main(argv=None):
         if args.host_inclusive == "on" or (args.host_inclusive == "auto" and world == 1):
             out["host_inclusive"] = host_inclusive(ctx, data, n, chunk, not args.sha1_only, args.segment_bytes,
                                                    batches[0])
-        if args.ingest_leg == "on" or (args.ingest_leg == "auto" and world == 1):
-            out["ingest_config"] = ingest_leg(args, rank, world, ctx, device, stream, MODE_AUTO)
+        if not args.sha1_only and (args.sha1_leg == "on" or (args.sha1_leg == "auto" and world == 1)):
+            out["sha1_only_config"] = sha1_only_leg(args, ctx, data, batches[0], device, stream)
+        if args.ingest_leg in ("on", "auto"):
+            out["ingest_config"] = ingest_leg(args, rank, world, ctx, device, stream, MODE_AUTO, dist)
         if args.uploads_leg == "on" or (args.uploads_leg == "auto" and world == 1):
             a = argparse.Namespace(**vars(args))
             a.upload_threads, a.uploads, a.open_per_thread, a.upload_bytes = 32, 8192, 256, 4 << 20
             out["uploads_path"] = uploads_workload(a, ctx)
         if args.receiver_leg == "on" or (args.receiver_leg == "auto" and world == 1):
             out["receiver_path"] = receiver_leg()
+        if args.drain_leg == "on" or (args.drain_leg == "auto" and world == 1):
+            out["drain_path"] = drain_leg()
         if args.concurrency_leg == "on" or (args.concurrency_leg == "auto" and world == 1):
             out["concurrency"] = concurrency_leg(args, ctx, device, stream)
         if args.mixed_leg == "on" or (args.mixed_leg == "auto" and world == 1):

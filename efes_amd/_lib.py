@@ -76,7 +76,13 @@ class Job(ctypes.Structure):
                 ("flags", ctypes.c_uint32), ("_reserved", ctypes.c_uint32)]
 
 
-assert ctypes.sizeof(Sha1State) == 104 and ctypes.sizeof(Job) == 56
+class QueueStats(ctypes.Structure):
+    """efes_queue_stats (ABI 5): what a queue's dispatcher launched, and its upload slots."""
+    _fields_ = [("launches", ctypes.c_uint64), ("jobs", ctypes.c_uint64), ("bytes", ctypes.c_uint64),
+                ("free_uploads", ctypes.c_uint32), ("max_uploads", ctypes.c_uint32)]
+
+
+assert ctypes.sizeof(Sha1State) == 104 and ctypes.sizeof(Job) == 56 and ctypes.sizeof(QueueStats) == 32
 
 # numpy mirrors for building arrays of jobs / states in bulk
 JOB_DTYPE = np.dtype([("data", "<u8"), ("length", "<u8"), ("sha1", "<u8"), ("crc32", "<u8"), ("sum", "<u8"),
@@ -119,6 +125,13 @@ SIGNATURES = {
     "efes_upload_state": (_I, [_VP, _P(Sha1State), _P(Crc32State)]),
     "efes_upload_sum": (_I, [_VP, _VP]),
     "efes_upload_close": (None, [_VP]),
+    "efes_queue_get_stats": (_I, [_VP, _P(QueueStats)]),
+    "efes_pool_create": (_I, [_P(_VP), _U32, _P(_VP)]),
+    "efes_pool_destroy": (None, [_VP]),
+    "efes_sha1_new_pool": (_I, [_VP, _P(_VP)]),
+    "efes_sha1_new_zero_pool": (_I, [_VP, _P(_VP)]),
+    "efes_crc32_new_pool": (_I, [_VP, _P(_VP)]),
+    "efes_pool_stats": (_I, [_VP, _U32, _P(QueueStats)]),
     "efes_sha1_new": (_I, [_VP, _P(_VP)]),
     "efes_sha1_new_zero": (_I, [_VP, _P(_VP)]),
     "efes_sha1_free": (None, [_VP]),

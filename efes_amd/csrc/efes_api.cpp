@@ -183,7 +183,7 @@ int efes_ctx_create(int device, efes_ctx** out) {
   ctx->cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
   hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming);
-  for (int i = 0; i < EFES_PLAN_MAX_PARTS - 1 && e == hipSuccess; ++i)
+  for (int i = 0; i < EFES_PLAN_MAX_PARTS && e == hipSuccess; ++i)
     e = hipStreamCreateWithFlags(&ctx->side[i], hipStreamNonBlocking);
   for (int i = 0; i < EFES_PLAN_MAX_PARTS && e == hipSuccess; ++i)
     e = hipEventCreateWithFlags(&ctx->ev_join[i], hipEventDisableTiming);
@@ -252,7 +252,7 @@ int efes_hash_submit_mode(efes_ctx* ctx, const efes_job* jobs, uint32_t njobs, v
   DeviceGuard g(ctx->device);
   hipStream_t s = pick(ctx, stream);
   if (mode == EFES_MODE_DEEP) return hip_err(efes::launch_deep(jobs, njobs, ctx->d_tabs, s));
-  if (mode == EFES_MODE_WIDE) return hip_err(efes::launch_wide(jobs, njobs, ctx->d_tabs, s));
+  if (mode == EFES_MODE_WIDE) return hip_err(efes::launch_wide(jobs, njobs, ctx->d_tabs, s, false, ctx->cus));
   if (mode == EFES_MODE_FED4 || mode == EFES_MODE_FED4E)
     return hip_err(efes::launch_fed(jobs, njobs, ctx->d_tabs, s, mode == EFES_MODE_FED4E));
   const int lanes = efes::group_of_mode(mode);

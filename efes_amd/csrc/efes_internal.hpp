@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <condition_variable>
+#include <list>
 #include <mutex>
 
 #include "../../include/efes_hash.h"
@@ -42,13 +44,27 @@ efes_sha1_state upload_shadow(const efes_upload* u);
 // The context's shared queue for the Go-surface digests, created on first use
 // (efes_stream.cpp); nullptr and *rc set on failure.
 efes_queue* stream_queue(efes_ctx* ctx, int* rc);
+// efes_upload_open that reports a full state-slot table as *no_slot (and EFES_ERR_NOMEM) so the
+// digest layer can evict an idle digest and retry instead of failing (efes_queue.cpp).
+int upload_open_slot(efes_queue* q, uint32_t hashes, const efes_sha1_state* sha1, const efes_crc32_state* crc32,
+                     efes_upload** out, bool* no_slot);
+uint32_t queue_free_slots(efes_queue* q);
+
+// Streaming digests (efes_stream.cpp) that hold an upload of a context's digest queue, oldest
+// first: the candidates for eviction when a digest needs a state slot and none is free.
+struct Digest;
+struct DigestRegistry {
+  std::mutex mu;
+  std::list<Digest*> open;
+  std::condition_variable released;  // a digest gave its upload back
+};
 
 // Launchers (host side, defined in efes_kernels.hip).
 hipError_t launch_deep(const efes_job* jobs, uint32_t njobs, const Tables* tabs, hipStream_t s);
 // exclusive: one workgroup (one wave per SIMD) per CU, so a long job's lane is never slowed by
 // other waves on its SIMD.
 hipError_t launch_wide(const efes_job* jobs, uint32_t njobs, const Tables* tabs, hipStream_t s,
-                       bool exclusive = false);
+                       bool exclusive = false, int cus = 256);
 // Grouped DEEP: 64/G jobs per wave, G in {4, 8, 16, 32} (64 = launch_deep).  exclusive: each
 // workgroup reserves all LDS of its CU, so no other workgroup shares the CU's SIMDs.
 hipError_t launch_group(const efes_job* jobs, uint32_t njobs, int G, const Tables* tabs, hipStream_t s,
@@ -112,15 +128,17 @@ struct efes_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   int cus = 256;                  // compute units (efes_plan_batch's capacity)
-  // streams of a planned batch's parts (efes_hash_submit_plan): side[0..2], then `stream`
-  hipStream_t side[EFES_PLAN_MAX_PARTS - 1] = {};
+  // streams of a planned batch's parts (efes_hash_submit_plan), one per part: never `stream`,
+  // so a planned batch does not queue behind NULL-stream work of the context
+  hipStream_t side[EFES_PLAN_MAX_PARTS] = {};
   hipEvent_t ev_fork = nullptr, ev_join[EFES_PLAN_MAX_PARTS] = {};
-  hipStream_t part_stream(uint32_t i) const { return i < EFES_PLAN_MAX_PARTS - 1 ? side[i] : stream; }
+  hipStream_t part_stream(uint32_t i) const { return side[i]; }
   std::mutex plan_mu;             // one planned submit at a time uses the side streams/events
   efes::Tables* d_tabs = nullptr;
   efes::SpanTables* d_span = nullptr;  // operators of the span CRC (efes_crc32_span)
   std::mutex mu;                  // guards the lazy creation of `digests`
   efes_queue* digests = nullptr;  // shared queue of the streaming digests (efes_stream.cpp)
+  efes::DigestRegistry dreg;      // the digests holding an upload of `digests`
 };
 
 namespace efes {

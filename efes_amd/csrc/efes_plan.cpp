@@ -374,17 +374,19 @@ int efes_hash_submit_plan(efes_ctx* ctx, const efes_job* jobs, const efes_plan* 
   efes::DeviceGuard guard(ctx->device);
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
   auto launch = [&](const efes_plan_part& p, const efes_job* first, hipStream_t st) {
-    if (p.mode == EFES_MODE_WIDE) return efes::launch_wide(first, p.jobs, ctx->d_tabs, st, p.exclusive != 0);
+    if (p.mode == EFES_MODE_WIDE) return efes::launch_wide(first, p.jobs, ctx->d_tabs, st, p.exclusive != 0, ctx->cus);
     if (p.mode == EFES_MODE_FED4 || p.mode == EFES_MODE_FED4E)
       return efes::launch_fed(first, p.jobs, ctx->d_tabs, st, p.mode == EFES_MODE_FED4E);
     return efes::launch_group(first, p.jobs, lanes_of(p.mode), ctx->d_tabs, st, p.exclusive != 0);
   };
   std::lock_guard<std::mutex> lk(ctx->plan_mu);
   // Fork: part i on the context's part stream i (longest jobs first, so their workgroups are
-  // placed first); join: `stream` waits for every part.  The part streams were created one after
-  // the other with the context, so they sit on distinct hardware queues (GPU_MAX_HW_QUEUES is 4):
-  // a part launched on the caller's stream instead could share a hardware queue with another
-  // part and not start before that one ends (seen in kernel traces: profiles/r02_mixtrace/).
+  // placed first); join: `stream` waits for every part.  Each part has a stream of its own, never
+  // the caller's or the context's NULL stream: a part launched on the caller's stream shared a
+  // hardware queue with another part in one trace and did not start before that one ended
+  // (profiles/r02_mixtrace/).  HIP assigns hardware queues (GPU_MAX_HW_QUEUES, 4 here)
+  // round-robin over every stream of the process, so distinct queues are likely -- the part
+  // streams are created one after the other -- but not guaranteed.
   if (plan->nparts == 1) return hip_err_plan(launch(plan->part[0], jobs, s));
   hipError_t e = hipEventRecord(ctx->ev_fork, s);
   const efes_job* first = jobs;

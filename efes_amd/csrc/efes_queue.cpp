@@ -50,6 +50,7 @@ struct efes_upload {
   uint32_t dslot = 0;            // device state slot
   int32_t cur = -1;              // staging chunk being filled (-1: none)
   uint64_t fill = 0;             // bytes in `cur`
+  uint64_t reserved = 0;         // bytes the last efes_upload_reserve granted (0: no reservation)
   uint64_t inflight = 0;         // chunks queued or running
   uint64_t queued = 0;           // of which still in q->pending (not in a launch yet)
   bool in_batch = false;         // has a chunk in the batch being assembled
@@ -91,6 +92,8 @@ struct efes_queue {
   int next_half = 0;
   bool stop = false;
   int fault = EFES_OK;
+  uint64_t n_launches = 0, n_jobs = 0, n_bytes = 0;  // efes_queue_get_stats
+  uint64_t n_attempts = 0, inject_at = 0;  // test hook: EFES_FAULT_INJECT_LAUNCH=k fails launch k
   std::thread th;
 
   void run();
@@ -180,7 +183,9 @@ void efes_queue::run() {
     if (e == hipSuccess) e = hipMemcpyAsync(dj, hj, sizeof(efes_job) * b.items.size(), hipMemcpyHostToDevice, stream);
     // DEEP (or grouped DEEP beyond one chunk per SIMD): efes::pcie_mode.
     const uint32_t nb = (uint32_t)b.items.size();
-    int rc = e == hipSuccess ? efes_hash_submit_mode(ctx, dj, nb, stream, efes::pcie_mode(ctx, nb)) : EFES_ERR_HIP;
+    int rc = e == hipSuccess ? EFES_OK : EFES_ERR_HIP;
+    if (rc == EFES_OK && inject_at && ++n_attempts == inject_at) rc = EFES_ERR_DEVICE_FAULT;  // as a faulted kernel
+    if (rc == EFES_OK) rc = efes_hash_submit_mode(ctx, dj, nb, stream, efes::pcie_mode(ctx, nb));
     if (rc == EFES_OK && hipEventCreateWithFlags(&b.ev, hipEventDisableTiming) != hipSuccess) rc = EFES_ERR_HIP;
     if (rc == EFES_OK && hipEventRecord(b.ev, stream) != hipSuccess) rc = EFES_ERR_HIP;
     lk.lock();
@@ -196,6 +201,9 @@ void efes_queue::run() {
       freed.notify_all();
       continue;
     }
+    ++n_launches;
+    n_jobs += b.items.size();
+    for (const Pending& p : b.items) n_bytes += p.len;
     running.push_back(std::move(b));
   }
 }
@@ -263,6 +271,9 @@ int efes_queue_create(efes_ctx* ctx, uint64_t chunk_bytes, uint32_t max_chunks, 
   q->max_uploads = max_uploads;
   const char* ah = getenv("EFES_QUEUE_AHEAD");
   q->ahead = ah && *ah ? strtoull(ah, nullptr, 10) : kAhead;
+  // Test hook (tests/test_gpu_boundary.py): the k-th launch of every queue created while it is set
+  // reports a device fault instead of running, as a kernel that faulted would.
+  if (const char* fi = getenv("EFES_FAULT_INJECT_LAUNCH")) q->inject_at = strtoull(fi, nullptr, 10);
   DeviceGuard g(ctx->device);
   hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&q->h_slab), q->chunk * max_chunks, hipHostMallocMapped);
   if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void**>(&q->z_slab), q->h_slab, 0);
@@ -311,6 +322,31 @@ void efes_queue_destroy(efes_queue* q) {
 
 int efes_upload_open(efes_queue* q, uint32_t hashes, const efes_sha1_state* sha1, const efes_crc32_state* crc,
                      efes_upload** out) {
+  bool no_slot = false;
+  return efes::upload_open_slot(q, hashes, sha1, crc, out, &no_slot);
+}
+
+int efes_queue_get_stats(efes_queue* q, efes_queue_stats* out) {
+  if (!q || !out) return EFES_ERR_ARG;
+  std::lock_guard<std::mutex> lk(q->mu);
+  out->launches = q->n_launches;
+  out->jobs = q->n_jobs;
+  out->bytes = q->n_bytes;
+  out->free_uploads = (uint32_t)q->free_states.size();
+  out->max_uploads = q->max_uploads;
+  return EFES_OK;
+}
+
+}  // extern "C"
+
+uint32_t efes::queue_free_slots(efes_queue* q) {
+  std::lock_guard<std::mutex> lk(q->mu);
+  return (uint32_t)q->free_states.size();
+}
+
+int efes::upload_open_slot(efes_queue* q, uint32_t hashes, const efes_sha1_state* sha1, const efes_crc32_state* crc,
+                           efes_upload** out, bool* no_slot) {
+  *no_slot = false;
   if (!q || !out || !hashes || (hashes & ~(EFES_HASH_SHA1 | EFES_HASH_CRC32))) return EFES_ERR_ARG;
   *out = nullptr;
   efes_upload* u = new (std::nothrow) efes_upload;
@@ -321,6 +357,7 @@ int efes_upload_open(efes_queue* q, uint32_t hashes, const efes_sha1_state* sha1
     std::lock_guard<std::mutex> lk(q->mu);
     if (q->free_states.empty()) {
       delete u;
+      *no_slot = true;
       return EFES_ERR_NOMEM;
     }
     u->dslot = q->free_states.back();
@@ -342,9 +379,12 @@ int efes_upload_open(efes_queue* q, uint32_t hashes, const efes_sha1_state* sha1
   return EFES_OK;
 }
 
+extern "C" {
+
 int efes_upload_write(efes_upload* u, const void* p, size_t n) {
   if (!u || (!p && n)) return EFES_ERR_ARG;
   if (u->latched) return u->latched;
+  u->reserved = 0;  // the bytes go where a reservation pointed
   const bool full_tail = u->shadow.nx == 64;
   const int rc = efes::replay_write(&u->shadow, static_cast<const uint8_t*>(p), n);
   if (rc) return u->latched = rc;  // the Go Write would panic (nx > 64)
@@ -388,9 +428,11 @@ int efes_upload_reserve(efes_upload* u, size_t min_bytes, void** p, size_t* n) {
   if (u->latched) return u->latched;
   efes_queue* q = u->q;
   const uint64_t want = std::max<uint64_t>(1, std::min<uint64_t>(min_bytes, q->chunk));
+  u->reserved = 0;
   if (u->cur >= 0 && q->chunk - u->fill < want) {  // too little room left: hand the chunk over
     std::unique_lock<std::mutex> lk(q->mu);
     enqueue_current(u, lk);
+    pace(u, lk);  // the same per-upload back-pressure as a chunk filled by write/commit
   }
   if (u->cur < 0) {
     std::unique_lock<std::mutex> lk(q->mu);
@@ -399,6 +441,7 @@ int efes_upload_reserve(efes_upload* u, size_t min_bytes, void** p, size_t* n) {
   }
   *p = q->h_slab + (size_t)u->cur * q->chunk + u->fill;
   *n = (size_t)(q->chunk - u->fill);
+  u->reserved = *n;
   return EFES_OK;
 }
 
@@ -407,7 +450,9 @@ int efes_upload_commit(efes_upload* u, size_t k) {
   if (u->latched) return u->latched;
   if (k == 0) return efes_upload_write(u, nullptr, 0);  // Write(empty): sha1.go:61-69 still runs
   efes_queue* q = u->q;
-  if (u->cur < 0 || k > q->chunk - u->fill) return EFES_ERR_ARG;  // not within the reserved room
+  // only bytes the last reserve granted, once: a stale pointer would hash stale staging bytes
+  if (u->cur < 0 || k > u->reserved || k > q->chunk - u->fill) return EFES_ERR_ARG;
+  u->reserved = 0;
   const uint8_t* src = q->h_slab + (size_t)u->cur * q->chunk + u->fill;
   const int rc = efes::replay_write(&u->shadow, src, k);
   if (rc) return u->latched = rc;  // the Go Write would panic (nx > 64)

@@ -23,7 +23,7 @@ import threading
 
 import numpy as np
 
-from ._lib import MODE_AUTO, EfesError, Plan, Sha1State, check, lib
+from ._lib import MODE_AUTO, EfesError, Plan, QueueStats, Sha1State, check, lib
 
 __all__ = ["Context", "default_context", "crc32_combine", "Sha1Digest", "CRC32Digest", "Sha1File", "Digest", "FileInfo",
            "new_sha1", "new_crc32_ieee", "EfesError"]
@@ -108,6 +108,30 @@ def default_context(device: int = 0) -> Context:
         return _contexts[device]
 
 
+class Pool:
+    """efes_pool (ABI 5): digests spread over several contexts (one process over every GPU,
+    server.go:130).  Each digest takes its upload slot, at every (re)open, on the context whose
+    digest queue has the most free slots."""
+
+    def __init__(self, ctxs):
+        self.ctxs = list(ctxs)
+        arr = (ctypes.c_void_p * len(self.ctxs))(*[c.handle.value for c in self.ctxs])
+        h = ctypes.c_void_p()
+        check(lib().efes_pool_create(arr, len(self.ctxs), ctypes.byref(h)), "efes_pool_create")
+        self.handle = h
+
+    def stats(self, i: int) -> QueueStats:
+        """Counters of the digest queue of context i (efes_pool_stats)."""
+        st = QueueStats()
+        check(lib().efes_pool_stats(self.handle, i, ctypes.byref(st)), "efes_pool_stats")
+        return st
+
+    def close(self) -> None:  # after every digest of the pool is freed
+        if self.handle:
+            lib().efes_pool_destroy(self.handle)
+            self.handle = None
+
+
 def crc32_combine(crc1: int, crc2: int, len2: int) -> int:
     """CRC-32 of A||B from crc(A), crc(B), |B| (efes_crc32_combine; crc32.go is GF(2)-linear)."""
     return int(lib().efes_crc32_combine(crc1 & 0xFFFFFFFF, crc2 & 0xFFFFFFFF, len2))
@@ -122,11 +146,16 @@ def _as_bytes(p) -> bytes:
 class Sha1Digest:
     """sha1digest (sha1.go:29-34) whose compressions run on the GPU."""
 
-    def __init__(self, ctx: Context | None = None, reset: bool = True):
-        self.ctx = ctx or default_context()
+    def __init__(self, ctx: Context | None = None, reset: bool = True, pool: Pool | None = None):
         h = ctypes.c_void_p()
-        fn = lib().efes_sha1_new if reset else lib().efes_sha1_new_zero
-        check(fn(self.ctx.handle, ctypes.byref(h)), "efes_sha1_new")
+        if pool is not None:  # the pool must outlive its digests: keep a reference
+            self.ctx, self.pool = None, pool
+            fn = lib().efes_sha1_new_pool if reset else lib().efes_sha1_new_zero_pool
+            check(fn(pool.handle, ctypes.byref(h)), "efes_sha1_new_pool")
+        else:
+            self.ctx, self.pool = ctx or default_context(), None
+            fn = lib().efes_sha1_new if reset else lib().efes_sha1_new_zero
+            check(fn(self.ctx.handle, ctypes.byref(h)), "efes_sha1_new")
         self._h = h
 
     def __del__(self):
@@ -177,10 +206,14 @@ class Sha1Digest:
 class CRC32Digest:
     """crc32digest (crc32.go:48-51) with the IEEE table, updated on the GPU."""
 
-    def __init__(self, ctx: Context | None = None):
-        self.ctx = ctx or default_context()
+    def __init__(self, ctx: Context | None = None, pool: Pool | None = None):
         h = ctypes.c_void_p()
-        check(lib().efes_crc32_new(self.ctx.handle, ctypes.byref(h)), "efes_crc32_new")
+        if pool is not None:
+            self.ctx, self.pool = None, pool
+            check(lib().efes_crc32_new_pool(pool.handle, ctypes.byref(h)), "efes_crc32_new_pool")
+        else:
+            self.ctx, self.pool = ctx or default_context(), None
+            check(lib().efes_crc32_new(self.ctx.handle, ctypes.byref(h)), "efes_crc32_new")
         self._h = h
 
     def __del__(self):
@@ -220,12 +253,12 @@ class CRC32Digest:
         check(lib().efes_crc32_unmarshal_text(self._h, t, len(t)), "CRC32Digest.unmarshal_text")
 
 
-def new_sha1(ctx: Context | None = None) -> Sha1Digest:  # sha1.go:48-52 NewSha1
-    return Sha1Digest(ctx)
+def new_sha1(ctx: Context | None = None, pool: Pool | None = None) -> Sha1Digest:  # sha1.go:48-52 NewSha1
+    return Sha1Digest(ctx, pool=pool)
 
 
-def new_crc32_ieee(ctx: Context | None = None) -> CRC32Digest:  # crc32.go:68 NewCRC32IEEE
-    return CRC32Digest(ctx)
+def new_crc32_ieee(ctx: Context | None = None, pool: Pool | None = None) -> CRC32Digest:  # crc32.go:68
+    return CRC32Digest(ctx, pool=pool)
 
 
 class Sha1File(io.RawIOBase):
@@ -285,9 +318,9 @@ class Sha1File(io.RawIOBase):
 class Digest:
     """fileinfo.go:15-18 `Digest{Sha1 *sha1digest "sha1"; CRC32 *crc32digest "crc32"}`."""
 
-    def __init__(self, ctx: Context | None = None):
-        self.sha1 = new_sha1(ctx)
-        self.crc32 = new_crc32_ieee(ctx)
+    def __init__(self, ctx: Context | None = None, pool: Pool | None = None):
+        self.sha1 = new_sha1(ctx, pool)
+        self.crc32 = new_crc32_ieee(ctx, pool)
 
     def write(self, p) -> int:
         """filereceiver.go:208 io.MultiWriter(f, CRC32, Sha1): CRC first, then SHA-1."""
@@ -305,17 +338,17 @@ class Digest:
 class FileInfo:
     """fileinfo.go:10-13 `FileInfo{Offset "offset"; Digest "digest"}` and its JSON file codec."""
 
-    def __init__(self, ctx: Context | None = None):  # fileinfo.go:20-27 newFileInfo
+    def __init__(self, ctx: Context | None = None, pool: Pool | None = None):  # fileinfo.go:20-27 newFileInfo
         self.offset = 0
-        self.digest = Digest(ctx)
+        self.digest = Digest(ctx, pool)
 
     def dumps(self) -> str:  # fileinfo.go:47-58 json.NewEncoder(f).Encode(fi)
         return json.dumps({"offset": self.offset, "digest": self.digest.to_json()}, separators=(",", ":")) + "\n"
 
     @classmethod
-    def loads(cls, s: str, ctx: Context | None = None) -> "FileInfo":  # fileinfo.go:37-45
+    def loads(cls, s: str, ctx: Context | None = None, pool: Pool | None = None) -> "FileInfo":  # fileinfo.go:37-45
         d = json.loads(s)
-        fi = cls(ctx)
+        fi = cls(ctx, pool)
         fi.offset = int(d["offset"])
         fi.digest.load_json(d["digest"])
         return fi

@@ -11,6 +11,8 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <memory>
 #include <vector>
 
@@ -662,11 +664,41 @@ struct FdGuard {
 };
 }  // namespace
 
+namespace {
+std::atomic<bool> g_phases_on{false};
+std::atomic<uint64_t> g_phase_ns[kPhases];
+const char* const kPhaseNames[kPhases] = {"create", "open", "reserve", "read", "write", "commit", "sync", "sum",
+                                          "info"};
+
+// Charges the time since the last mark to a phase (when enabled).
+struct PhaseClock {
+  bool on = g_phases_on.load(std::memory_order_relaxed);
+  std::chrono::steady_clock::time_point t = on ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point{};
+  void mark(SavePhase p) {
+    if (!on) return;
+    const auto now = std::chrono::steady_clock::now();
+    g_phase_ns[p].fetch_add((uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(now - t).count(),
+                            std::memory_order_relaxed);
+    t = now;
+  }
+};
+}  // namespace
+
+void EnableSavePhases(bool on) {
+  for (auto& v : g_phase_ns) v.store(0, std::memory_order_relaxed);
+  g_phases_on.store(on, std::memory_order_relaxed);
+}
+void SavePhaseTotals(uint64_t ns[kPhases]) {
+  for (int p = 0; p < kPhases; ++p) ns[p] = g_phase_ns[p].load(std::memory_order_relaxed);
+}
+const char* SavePhaseName(int p) { return p >= 0 && p < kPhases ? kPhaseNames[p] : "?"; }
+
 Error saveFile(Hasher* h, const std::string& path, int64_t offset, int64_t length, Reader& r, int64_t* new_offset,
                bool* done, DigestSums* sums) {  // filereceiver.go:171-227
   *new_offset = 0;
   *done = false;
   FileInfo fi;
+  PhaseClock pc;
   // A receiver without a GPU context (h == nullptr) fails every request that would hash, before
   // touching the file: there is no CPU fallback.  Offset mismatches are still reported first.
   if (offset == 0) {
@@ -674,6 +706,7 @@ Error saveFile(Hasher* h, const std::string& path, int64_t offset, int64_t lengt
     Error e = createFile(path);  // a PATCH at 0 needs no prior POST (filereceiver.go:175)
     if (e) return e;
     fi = newFileInfo();
+    pc.mark(kPhaseCreate);
   } else {
     Error e = ReadFileInfo(path, &fi);
     if (e) return e;
@@ -699,6 +732,7 @@ Error saveFile(Hasher* h, const std::string& path, int64_t offset, int64_t lengt
   g.held = true;
   int rc = efes_upload_open(h->queue(g.dev), EFES_HASH_SHA1 | EFES_HASH_CRC32, &fi.Sha1, &fi.CRC32, &g.u);
   if (rc) return lib_error(rc);
+  pc.mark(kPhaseOpen);
 
   // n, _ := io.Copy(w, r) (filereceiver.go:209): 32 KiB buffers; a read error ends the copy
   // and is ignored, so the bytes read so far still advance the state.  The buffer IS the
@@ -711,18 +745,22 @@ Error saveFile(Hasher* h, const std::string& path, int64_t offset, int64_t lengt
     size_t room = 0;
     rc = efes_upload_reserve(g.u, kCopyBuf, &sp, &room);
     if (rc) return lib_error(rc);  // the .info keeps its old offset
+    pc.mark(kPhaseReserve);
     uint8_t* buf = static_cast<uint8_t*>(sp);
     Error er;
     const size_t nr = r.Read(buf, std::min(room, kCopyBuf), &er);
+    pc.mark(kPhaseRead);
     if (nr > 0) {
       size_t nw = 0;
       Error ew = write_full(f.fd, path, buf, nr, &nw);
+      pc.mark(kPhaseWrite);
       if (ew) {  // MultiWriter stops at the file: the digests never see this buffer
         n += (int64_t)nw;
         break;
       }
       rc = efes_upload_commit(g.u, nr);  // CRC32.Write, Sha1.Write
       if (rc) return lib_error(rc);
+      pc.mark(kPhaseCommit);
       n += (int64_t)nr;
     }
     if (er) break;
@@ -731,6 +769,7 @@ Error saveFile(Hasher* h, const std::string& path, int64_t offset, int64_t lengt
   const int fd = f.fd;
   f.fd = -1;
   if (::close(fd) != 0) return errno_error("close", path, errno);
+  pc.mark(kPhaseSync);
 
   fi.Offset = offset + n;
   *new_offset = fi.Offset;
@@ -738,14 +777,20 @@ Error saveFile(Hasher* h, const std::string& path, int64_t offset, int64_t lengt
     uint8_t s[24];
     rc = efes_upload_sum(g.u, s);  // Sha1.Sum(nil) || CRC32.Sum(nil) (filereceiver.go:99-100)
     if (rc) return lib_error(rc);
+    pc.mark(kPhaseSum);
     memcpy(sums->sha1, s, 20);
     memcpy(sums->crc32, s + 20, 4);
     *done = true;
-    return DeleteFileInfo(path);
+    Error e = DeleteFileInfo(path);
+    pc.mark(kPhaseInfo);
+    return e;
   }
   rc = efes_upload_state(g.u, &fi.Sha1, &fi.CRC32);  // MarshalText's input after the Writes
   if (rc) return lib_error(rc);
-  return SaveFileInfo(path, fi);  // filereceiver.go:226
+  pc.mark(kPhaseSum);
+  Error e = SaveFileInfo(path, fi);  // filereceiver.go:226
+  pc.mark(kPhaseInfo);
+  return e;
 }
 
 // ---- strconv / filepath / net/http -------------------------------------------------------------

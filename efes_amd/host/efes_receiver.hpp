@@ -158,6 +158,25 @@ Error saveFile(Hasher* h, const std::string& path, int64_t offset, int64_t lengt
                int64_t* new_offset, bool* done, DigestSums* sums);
 std::string OffsetMismatchText(int64_t given, int64_t required);  // OffsetMismatchError.Error()
 
+// Host-time accounting of saveFile by phase (tools/bench_receiver, EFES_RECEIVER_PHASES=1):
+// nanoseconds summed over every request, per phase.  Off by default (one branch per phase);
+// when on, one steady_clock read and one relaxed atomic add per phase.
+enum SavePhase {
+  kPhaseCreate,   // createFile: os.Create + Close + the newFileInfo .info (filereceiver.go:148-165)
+  kPhaseOpen,     // ReadFileInfo / OpenFile / Seek / upload slot + efes_upload_open
+  kPhaseReserve,  // efes_upload_reserve (waits for a staging chunk, hands full ones over)
+  kPhaseRead,     // r.Read into the staging buffer (the socket's copy)
+  kPhaseWrite,    // write(2) of the buffer to the file
+  kPhaseCommit,   // efes_upload_commit (Go's x/nx/len replay; hands a full chunk over)
+  kPhaseSync,     // f.Sync() + Close
+  kPhaseSum,      // efes_upload_sum / efes_upload_state: waiting for this upload's GPU jobs
+  kPhaseInfo,     // DeleteFileInfo / SaveFileInfo at the end
+  kPhases
+};
+void EnableSavePhases(bool on);
+void SavePhaseTotals(uint64_t ns[kPhases]);
+const char* SavePhaseName(int p);
+
 // strconv.ParseInt(s, 10, 64)
 Error ParseInt(std::string_view s, int64_t* out);
 // filepath.Join(dir, p) (Clean of the joined path)

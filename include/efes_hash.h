@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define EFES_ABI_VERSION 4
+#define EFES_ABI_VERSION 5
 
 /* ---- error codes ---------------------------------------------------------------- */
 #define EFES_OK 0
@@ -146,14 +146,17 @@ int efes_auto_mode(const efes_ctx* ctx, uint32_t njobs);
  * efes_plan_batch orders the jobs longest-first (order[i] = index into `lengths` of the job to
  * place at jobs_device[i]) and picks the cuts, shapes and exclusivity from an issue-time model
  * of the kernels calibrated on MI355X; efes_hash_submit_plan launches a batch
- * laid out in that order: each part on a stream of the context (distinct hardware queues), after
- * the work queued on `stream`, which then waits for all of them.  Planning is host-only (no device access; ctx
+ * laid out in that order: each part on a part stream of its own (created one after the other, so
+ * usually -- HIP assigns hardware queues round-robin over all streams of the process, so not
+ * certainly -- on distinct hardware queues), after the work queued on `stream`, which then waits
+ * for all of them.  Planning is host-only (no device access; ctx
  * may be NULL: then the capacity of one MI355X, 256 CUs, is assumed). */
 #define EFES_PLAN_MAX_PARTS 4
 typedef struct efes_plan_part {
     uint32_t jobs;       /* consecutive jobs of this part (in plan order) */
-    int32_t mode;        /* EFES_MODE_DEEP, EFES_MODE_GROUPn or EFES_MODE_WIDE */
-    uint32_t exclusive;  /* 1: each workgroup reserves its CU (one wave per SIMD) */
+    int32_t mode;        /* EFES_MODE_DEEP, EFES_MODE_GROUPn, EFES_MODE_FED4, EFES_MODE_FED4E or EFES_MODE_WIDE */
+    uint32_t exclusive;  /* 1: each workgroup reserves its CU (one wave per SIMD); FED4/FED4E parts
+                            ignore it: their workgroups always own their CU */
     uint32_t _reserved;
 } efes_plan_part;
 typedef struct efes_plan {
@@ -233,22 +236,46 @@ int efes_upload_write(efes_upload* u, const void* p, size_t n);
  * dispatcher first; blocks while every chunk is in use).  Fill k <= *n of them -- read a request
  * body straight in, write the file from there -- and efes_upload_commit(u, k): the same as
  * efes_upload_write of those k bytes (one Write of k bytes, sha1.go:58-79) without the copy.
- * Bytes reserved but not committed are dropped; reserve again before the next commit. */
+ * Bytes reserved but not committed are dropped; reserve again before the next commit (a commit
+ * of more bytes than the last reserve granted, a second commit, or a commit after a write returns
+ * EFES_ERR_ARG).  The pointer is valid only until the commit. */
 int efes_upload_reserve(efes_upload* u, size_t min_bytes, void** p, size_t* n);
 int efes_upload_commit(efes_upload* u, size_t k);
 int efes_upload_flush(efes_upload* u);
 int efes_upload_state(efes_upload* u, efes_sha1_state* sha1, efes_crc32_state* crc32);
 int efes_upload_sum(efes_upload* u, uint8_t out[24]);
 void efes_upload_close(efes_upload* u); /* drops bytes staged since the last sync point */
+/* Counters of a queue (ABI 5): what its dispatcher launched, and its upload slots. */
+typedef struct efes_queue_stats {
+    uint64_t launches;      /* kernel launches */
+    uint64_t jobs;          /* jobs in them (one per upload per launch, Sums included) */
+    uint64_t bytes;         /* staged bytes hashed */
+    uint32_t free_uploads;  /* upload (state) slots free now */
+    uint32_t max_uploads;
+} efes_queue_stats;
+int efes_queue_get_stats(efes_queue* q, efes_queue_stats* out);
 
 /* ---- layer 2: streaming digests mirroring the Go surface ----------------------------
  * Each object is an upload (above) of the context's shared digest queue that keeps only its
  * own hash, so unchanged Go code -- MultiWriter(f, CRC32, Sha1) in every request goroutine --
  * is batched across all concurrent requests: Write stages into pinned memory and returns,
  * Sum / Sum32 / MarshalText are the sync points.  The shared queue holds
- * EFES_DIGEST_STAGING_MIB (env, default 256) of pinned staging in 64 KiB chunks; a Write
- * blocks while all chunks are in flight, and EFES_ERR_NOMEM is returned when more digests
- * are being written at once than the pool has chunks. */
+ * EFES_DIGEST_STAGING_MIB (env, default 256) of pinned staging in 64 KiB chunks (an upload slot
+ * per chunk but one); a Write blocks while all chunks are in flight.
+ *
+ * Go's Write never fails (sha1.go:58-79, crc32.go:76-86), and neither does this one for any
+ * number of live digests:
+ *   - a digest holds an upload slot only between its first Write and its next sync point: every
+ *     Sum / Sum32 / MarshalText parks the state on the host and gives the slot back, the next
+ *     Write takes one again (so digests that are never freed hold no queue resources);
+ *   - a Write (or Sum) that finds every slot taken evicts the oldest digest that is not inside a
+ *     call (its staged bytes are hashed, its state parked on the host) and takes its slot; if all
+ *     holders are inside calls it waits for one of them -- back-pressure, never EFES_ERR_NOMEM;
+ *   - a device or HIP fault during a Write is latched and the Write returns EFES_OK: the next
+ *     Sum / Sum32 / MarshalText reports it (MarshalText's error -> HTTP 500, filereceiver.go:94-96).
+ * Write returns an error only for bad arguments and for the states on which Go's Write panics
+ * (EFES_ERR_STATE: nx > 64, sha1.go:62).  The object itself is host memory, so freeing it late
+ * (a Go finalizer) costs nothing scarce. */
 typedef struct efes_sha1 efes_sha1;
 typedef struct efes_crc32 efes_crc32;
 
@@ -266,6 +293,21 @@ int efes_sha1_get_state(efes_sha1* d, efes_sha1_state* out);
 int efes_sha1_set_state(efes_sha1* d, const efes_sha1_state* in);
 
 int efes_crc32_new(efes_ctx* ctx, efes_crc32** out);                     /* crc32.go:68 NewCRC32IEEE */
+
+/* Multi-GPU digests (ABI 5).  A storage server is one process (server.go:130, one goroutine per
+ * request), so one process's digests should use every GPU: a pool spreads them over its
+ * contexts.  A pooled digest takes its upload slot, at every (re)open, on the context whose digest
+ * queue has the most free slots (its state is on the host between sync points, so consecutive
+ * PATCHes of one object may run on different GPUs; the byte order is kept by the caller).  The
+ * contexts must outlive the pool, and the pool its digests. */
+typedef struct efes_pool efes_pool;
+int efes_pool_create(efes_ctx* const* ctxs, uint32_t n, efes_pool** out);
+void efes_pool_destroy(efes_pool* p);
+int efes_sha1_new_pool(efes_pool* p, efes_sha1** out);                   /* NewSha1 on the pool */
+int efes_sha1_new_zero_pool(efes_pool* p, efes_sha1** out);              /* `var d sha1digest` on the pool */
+int efes_crc32_new_pool(efes_pool* p, efes_crc32** out);                 /* NewCRC32IEEE on the pool */
+/* Counters of the digest queue of the pool's i-th context (zeros before its first digest Write). */
+int efes_pool_stats(efes_pool* p, uint32_t i, efes_queue_stats* out);
 void efes_crc32_free(efes_crc32* d);
 void efes_crc32_reset(efes_crc32* d);                                    /* crc32.go:74 */
 int efes_crc32_size(void);                                               /* crc32.go:70 (4) */

@@ -1,0 +1,260 @@
+"""The Go-surface boundary under load (efes_hash.h layer 2, ABI 5), against the CPU oracle.
+
+Go's sha1digest.Write / crc32digest.Write never fail (sha1.go:58-79, crc32.go:76-86), and
+filereceiver.go creates two fresh digests per PATCH (fileinfo.go:20-27, filereceiver.go:180-182)
+that only the garbage collector frees.  These tests hold that contract with a deliberately tiny
+digest queue (EFES_DIGEST_STAGING_MIB=1: 16 staging chunks, 15 upload slots):
+  * 200 PATCHes, each through a NEW FileInfo that is never freed until the end;
+  * more digests written-but-not-synced at once than there are slots (eviction), from 16 threads;
+  * a device fault in the middle of a Write stream: Write still returns len(p), the sync points
+    report the fault (MarshalText -> HTTP 500, filereceiver.go:94-96);
+and the multi-GPU pool (efes_pool_*): 16 request threads' digests spread over two contexts
+(standing in for two GPUs), both queues doing work, every text and Sum equal to the oracle's.
+"""
+import hashlib
+import json
+import random
+import threading
+import zlib
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import efes_amd
+    from efes_amd import hashing
+    return dict(efes=efes_amd, hashing=hashing)
+
+
+@pytest.fixture
+def small_ctx(gpu, monkeypatch):
+    """A fresh context whose digest queue (created at its first digest Write) has 15 upload slots."""
+    monkeypatch.setenv("EFES_DIGEST_STAGING_MIB", "1")
+    ctx = gpu["hashing"].Context(0)
+    yield ctx
+    ctx.close()
+
+
+def _payload(n: int, seed: int) -> bytes:
+    return random.Random(seed).randbytes(n)
+
+
+class OracleObject:
+    """The reference's digests of one object (oracle = C restatement of sha1.go / crc32.go)."""
+
+    def __init__(self, oracle):
+        self.sha = oracle.Sha1()
+        self.crc = oracle.Crc32()
+
+    def write(self, p: bytes, piece: int = 32 << 10):
+        """The same Write calls _patch makes (Go's stale x bytes follow the Write boundaries), in
+        MultiWriter order (filereceiver.go:208): CRC32, then Sha1."""
+        for k in range(0, len(p), piece):
+            self.crc.write(p[k:k + piece])
+            assert self.sha.write(p[k:k + piece]) == 0
+
+    def info(self, offset: int) -> str:  # fileinfo.go:47-58
+        return json.dumps({"offset": offset, "digest": {"sha1": self.sha.marshal_text(),
+                                                          "crc32": self.crc.marshal_text()}},
+                          separators=(",", ":")) + "\n"
+
+
+def _patch(hashing, fi, body: bytes, write: int = 32 << 10):
+    """saveFile's io.Copy(MultiWriter(f, CRC32, Sha1), r) in `write`-byte reads (filereceiver.go:209)."""
+    for k in range(0, len(body), write):
+        n = fi.digest.write(body[k:k + write])
+        assert n == len(body[k:k + write])  # Write returns len(p), nil
+
+
+def test_200_patches_new_fileinfo_each_never_freed(gpu, small_ctx, oracle):
+    """The verdict's scenario: 20 objects x 10 PATCHes = 200 PATCHes, interleaved; every PATCH
+    builds a NEW FileInfo from the saved .info text (or newFileInfo for the first), streams its
+    body, then saves the .info (MarshalText) or, on the last PATCH, reads the Sums.  No FileInfo
+    is freed before the end.  Every Write succeeds; every .info text and Sum equals the oracle's."""
+    hashing = gpu["hashing"]
+    pool1 = hashing.Pool([small_ctx])  # only to read the digest queue's counters
+    objs = 20
+    bodies = {o: [_payload(random.Random(o * 100 + p).choice([1, 63, 64, 65, 4097, 40000, 65536, 70001, 131072]),
+                           o * 1000 + p) for p in range(10)] for o in range(objs)}
+    saved = {o: None for o in range(objs)}
+    expect = {o: OracleObject(oracle) for o in range(objs)}
+    offset = {o: 0 for o in range(objs)}
+    alive = []  # every FileInfo of every PATCH, freed only at the end (the GC never ran)
+    for p in range(10):
+        for o in range(objs):
+            fi = (hashing.FileInfo(small_ctx) if saved[o] is None
+                  else hashing.FileInfo.loads(saved[o], small_ctx))  # filereceiver.go:172-182
+            alive.append(fi)
+            body = bodies[o][p]
+            _patch(hashing, fi, body)
+            expect[o].write(body)
+            offset[o] += len(body)
+            fi.offset = offset[o]
+            if p < 9:
+                saved[o] = fi.dumps()  # SaveFileInfo (filereceiver.go:226)
+                assert saved[o] == expect[o].info(offset[o]), (o, p)
+            else:  # the upload is complete: the digest headers (filereceiver.go:99-100)
+                data = b"".join(bodies[o])
+                assert fi.digest.sha1.sum() == hashlib.sha1(data).digest()
+                assert fi.digest.crc32.sum32() == zlib.crc32(data)
+                assert fi.digest.sha1.marshal_text().decode() == expect[o].sha.marshal_text()
+    st = pool1.stats(0)
+    assert st.max_uploads == 15 and st.free_uploads == 15  # every digest is parked after its sync point
+    assert st.jobs > 0 and st.bytes == sum(len(b) for bs in bodies.values() for b in bs) * 2
+    del alive
+    pool1.close()
+
+
+def test_more_unsynced_digests_than_slots_evict(gpu, small_ctx, oracle):
+    """48 digests written to and NOT synced (as a failed saveFile abandons them to the GC) on a queue
+    with 15 upload slots: every Write succeeds -- the oldest idle holder is evicted (its staged
+    bytes hashed, its state parked on the host) -- and each digest, synced later, equals the oracle."""
+    hashing = gpu["hashing"]
+    n = 48
+    digests = [hashing.Digest(small_ctx) for _ in range(n)]
+    exp = [OracleObject(oracle) for _ in range(n)]
+    rng = random.Random(3)
+    for r in range(3):  # three rounds of Writes over all of them, never a sync point in between
+        for i in range(n):
+            p = _payload(rng.choice([5, 64, 1000, 33000, 65536, 65537]), r * 100 + i)
+            assert digests[i].write(p) == len(p)
+            exp[i].write(p, piece=len(p) or 1)
+    for i in reversed(range(n)):
+        assert digests[i].sha1.marshal_text().decode() == exp[i].sha.marshal_text(), i
+        assert digests[i].crc32.marshal_text().decode() == exp[i].crc.marshal_text(), i
+        rc, d = exp[i].sha.sum()
+        assert rc == 0 and digests[i].sha1.sum() == d
+
+
+def test_concurrent_threads_more_digests_than_slots(gpu, small_ctx, oracle):
+    """16 request threads x 6 open objects each (96 digests on 15 slots), 32 KiB Writes in
+    MultiWriter order with a sync point only every third PATCH: no Write fails or deadlocks, and
+    every .info text and final Sum equals the oracle's."""
+    hashing = gpu["hashing"]
+    errors = []
+
+    def worker(t):
+        try:
+            rng = random.Random(t)
+            objs = [(hashing.FileInfo(small_ctx), OracleObject(oracle), []) for _ in range(6)]
+            for p in range(6):
+                for k, (fi, ex, parts) in enumerate(objs):
+                    body = _payload(rng.choice([100, 32768, 50000, 65536, 98304]), t * 1000 + p * 10 + k)
+                    _patch(hashing, fi, body)
+                    ex.write(body)
+                    parts.append(body)
+                    if p % 3 == 2:
+                        txt = fi.digest.to_json()
+                        assert txt == {"sha1": ex.sha.marshal_text(), "crc32": ex.crc.marshal_text()}, (t, p, k)
+            for fi, ex, parts in objs:
+                data = b"".join(parts)
+                assert fi.digest.sha1.sum() == hashlib.sha1(data).digest(), t
+                assert fi.digest.crc32.sum32() == zlib.crc32(data), t
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(repr(e))
+
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(16)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join(timeout=100)
+    assert not any(th.is_alive() for th in ths), "a digest call deadlocked"
+    assert not errors, errors[:3]
+
+
+def test_device_fault_is_latched_to_the_sync_point(gpu, monkeypatch, oracle):
+    """A device fault under the Writes (EFES_FAULT_INJECT_LAUNCH=1: the queue's first launch reports
+    a fault, as a faulted kernel would): every Write keeps returning len(p) -- Go's Write never
+    fails -- and MarshalText / Sum report the fault (MarshalText's error -> HTTP 500).  The queue
+    stays faulted, as after a real device fault (a new digest there also fails at its sync point),
+    while a digest on a healthy context is unaffected."""
+    hashing, efes = gpu["hashing"], gpu["efes"]
+    monkeypatch.setenv("EFES_FAULT_INJECT_LAUNCH", "1")
+    ctx = hashing.Context(0)
+    d = d2 = None
+    try:
+        d = hashing.Digest(ctx)
+        assert d.write(b"x") == 1  # creates the context's digest queue while the hook is set
+        monkeypatch.delenv("EFES_FAULT_INJECT_LAUNCH")
+        for k in range(8):
+            assert d.write(_payload(65536 + k, 10 + k)) == 65536 + k
+        with pytest.raises(efes.EfesError) as e:
+            d.sha1.marshal_text()
+        assert e.value.code in (efes.EFES_ERR_DEVICE_FAULT, efes.EFES_ERR_HIP)
+        with pytest.raises(efes.EfesError):
+            d.sha1.sum()
+        with pytest.raises(efes.EfesError):
+            d.crc32.marshal_text()
+        assert d.write(b"more") == 4  # still no Write error
+        d.sha1.reset()  # Reset clears the object's latch; the queue is still faulted
+        assert d.sha1.write(b"abc") == 3
+        with pytest.raises(efes.EfesError):
+            d.sha1.marshal_text()
+        d2 = hashing.Digest()  # the default (healthy) context
+        body = _payload(100000, 99)
+        d2.write(body)
+        assert d2.sha1.marshal_text().decode() == _oracle_text(oracle, body)
+        assert d2.crc32.sum32() == zlib.crc32(body)
+    finally:
+        del d, d2
+        ctx.close()
+
+
+def _oracle_text(oracle, data: bytes) -> str:
+    o = oracle.Sha1()
+    o.write(data)
+    return o.marshal_text()
+
+
+def test_pool_spreads_digests_over_contexts(gpu, oracle):
+    """efes_pool over two contexts (two queues, standing in for two GPUs of one process): 16 request
+    threads run resumable uploads PATCH by PATCH through pooled FileInfo digests (UnmarshalText of
+    the saved .info -> 32 KiB Writes in MultiWriter order -> MarshalText, Sum at the end).  Both
+    contexts' digest queues launch work, and every text and digest equals the oracle's."""
+    hashing = gpu["hashing"]
+    ctxs = [hashing.Context(0), hashing.Context(0)]
+    pool = hashing.Pool(ctxs)
+    errors = []
+
+    def worker(t):
+        try:
+            rng = random.Random(50 + t)
+            for obj in range(3):
+                ex, parts, saved, off = OracleObject(oracle), [], None, 0
+                for p in range(4):
+                    fi = hashing.FileInfo(pool=pool) if saved is None else hashing.FileInfo.loads(saved, pool=pool)
+                    body = _payload(rng.choice([1, 4096, 65536, 200000, 1 << 20]), t * 100 + obj * 10 + p)
+                    _patch(hashing, fi, body)
+                    ex.write(body)
+                    parts.append(body)
+                    off += len(body)
+                    fi.offset = off
+                    if p < 3:
+                        saved = fi.dumps()
+                        assert saved == ex.info(off), (t, obj, p)
+                    else:
+                        data = b"".join(parts)
+                        assert fi.digest.sha1.sum() == hashlib.sha1(data).digest()
+                        assert fi.digest.crc32.sum32() == zlib.crc32(data)
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(repr(e))
+
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(16)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join(timeout=100)
+    assert not any(th.is_alive() for th in ths)
+    assert not errors, errors[:3]
+    s0, s1 = pool.stats(0), pool.stats(1)
+    assert s0.jobs > 0 and s1.jobs > 0, (s0.jobs, s1.jobs)
+    assert s0.bytes + s1.bytes > 0
+    pool.close()
+    for c in ctxs:
+        c.close()

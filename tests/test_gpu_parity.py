@@ -659,6 +659,19 @@ def test_upload_reserve_commit_equals_write(env, oracle):
         with pytest.raises(efes.EfesError) as e:
             up.commit(len(view) + 1)
         assert e.value.code == efes.EFES_ERR_ARG
+        # a reservation is good for ONE commit: a second one (a stale pointer) is refused, and so is a
+        # commit after a write
+        view = up.reserve(64)
+        view[:8] = b"12345678"
+        up.commit(8)
+        with pytest.raises(efes.EfesError) as e:
+            up.commit(8)
+        assert e.value.code == efes.EFES_ERR_ARG
+        up.reserve(64)
+        up.write(b"x")
+        with pytest.raises(efes.EfesError) as e:
+            up.commit(1)
+        assert e.value.code == efes.EFES_ERR_ARG
         up.close()
 
 
@@ -959,6 +972,37 @@ def test_planned_batch_forced_parts(env, oracle, force, monkeypatch):
         assert shas[i] == hashlib.sha1(dat).hexdigest() and crcs[i] == zlib.crc32(dat), (force, i)
 
 
+@pytest.mark.parametrize("force", ["1:32x,2:48x,4:40x", "2:20x,64:3x,1:16x", "1:40x,2:40x,8:20x,0:60"])
+def test_planned_batch_four_parts_fed_on_torch_stream(env, oracle, force, monkeypatch):
+    """Plans of four parts with FED lanes (FED4 = 1, FED4E = 2) beside grouped / DEEP / WIDE parts,
+    submitted on a non-null torch stream (so the caller's stream is neither the context's nor a
+    part stream): every part runs on its own part stream, forked from and joined back into the
+    caller's stream, and every job matches hashlib/zlib."""
+    from efes_amd.batch import MODE_PLAN
+    torch = env["torch"]
+    rng = np.random.default_rng(11)
+    n = 160
+    lengths = (np.asarray([32 << 10 << int(k) for k in rng.integers(0, 5, n)]) // 8 + rng.integers(0, 100, n))
+    offsets = np.concatenate([[0], np.cumsum(lengths)[:-1]]).astype(np.uint64)
+    host = oracle.fill_synthetic(int(lengths.sum()) + 8, 78)
+    buf = device_buffer(env, host)
+    monkeypatch.setenv("EFES_PLAN_FORCE", force)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        b = env["DeviceBatch"](buf.data_ptr(), offsets, lengths, fresh=True, ctx=env["ctx"])
+        b.make_plan()
+        assert b.plan.nparts == 4 and sum(p[0] for p in b.plan.parts()) == n
+        assert b.stream() != 0 and b.stream() != env["ctx"].stream
+        b.submit(MODE_PLAN)
+        st = b.status.cpu()  # ordered on s after the plan's join
+    torch.cuda.synchronize()
+    assert (st.numpy()[:n] == 0).all()
+    shas, crcs = b.sha1_hex(), b.crc_sum()
+    for i in range(n):
+        dat = host[int(offsets[i]):int(offsets[i]) + int(lengths[i])].tobytes()
+        assert shas[i] == hashlib.sha1(dat).hexdigest() and crcs[i] == zlib.crc32(dat), (force, i)
+
+
 def test_planned_batch_random_lengths(env, oracle):
     """The planner's own plan (no forcing) on a heavy-tailed length mix: every digest correct."""
     from efes_amd.batch import MODE_PLAN
@@ -1010,6 +1054,35 @@ def test_full_size_metric_config_all_shapes_agree(env):
     assert (got["deep"][1] == got["group32"][1]).all() and (got["deep"][1] == got["wide"][1]).all()
     assert len(set(got["deep"][0])) == n  # distinct data per chunk
     _spot_check(env, buf, offsets, lengths, got["deep"][0], got["deep"][1], [0, 1, 511, 1022, 1023])
+
+
+@pytest.mark.parametrize("mode_name", ["deep", "auto"])
+def test_full_size_config1_sha1_only(env, mode_name):
+    """BASELINE configs[1] at full size: 1024 x 4 MiB, SHA-1 ONLY (jobs without a CRC state, so
+    DEEP's producer runs its do_crc == false branch over whole 4 MiB chunks), device-filled like
+    bench.py --sha1-only.  Its digests equal the fused run's SHA-1 digests (and hashlib on spot
+    chunks), the Sums' CRC bytes stay zero, and no CRC state is written."""
+    torch = env["torch"]
+    n, size = 1024, 4 << 20
+    buf = torch.empty(n * size, dtype=torch.uint8, device="cuda:0")
+    env["ctx"].fill_synthetic(buf.data_ptr(), buf.numel(), 0xEFE5, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    offsets, lengths = np.arange(n, dtype=np.uint64) * size, np.full(n, size, np.uint64)
+    mode = env["efes"].MODE_DEEP if mode_name == "deep" else env["efes"].MODE_AUTO
+    sha_only = env["DeviceBatch"](buf.data_ptr(), offsets, lengths, crc32=False, fresh=True, ctx=env["ctx"])
+    sha_only.crcs.fill_(0x5A)  # a CRC state the jobs do not own must stay untouched
+    torch.cuda.synchronize()
+    sha_only.run(mode)
+    assert (sha_only.status_host() == 0).all()
+    fused = env["DeviceBatch"](buf.data_ptr(), offsets, lengths, fresh=True, ctx=env["ctx"])
+    fused.run(mode)
+    assert sha_only.sha1_hex() == fused.sha1_hex()
+    assert (sha_only.sums_host()[:, 20:] == 0).all()
+    assert (sha_only.crcs.cpu().numpy() == 0x5A).all()
+    shas = sha_only.sha1_hex()
+    for i in (0, 1, 777, 1023):
+        d = buf[i * size:(i + 1) * size].cpu().numpy().tobytes()
+        assert shas[i] == hashlib.sha1(d).hexdigest(), i
 
 
 def test_full_size_mixed_config_plan_equals_wide(env):

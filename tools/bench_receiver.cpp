@@ -9,11 +9,18 @@
 //                                 (gpus > 1: one process over several GPUs, a queue per GPU, each
 //                                  PATCH on the least-loaded one -- a storage server is one process)
 //   tools/bench_receiver sha1file <dir> <threads> <files_per_thread> <file_bytes>
+//   tools/bench_receiver drain    <dir> <workers> <fids> <file_bytes> [nfiles]  (the drainer's read-back,
+//                                 drain.go:87-125: <fids> moves of the existing files <dir>/<i % nfiles>.fid
+//                                 (nfiles defaults to fids), each moved by
+//                                 write.go's sendFile -- read through Sha1File, hashed on the GPU,
+//                                 one PATCH per ChunkSize -- to a sink server; <workers> files in
+//                                 flight at once, their hashing batched by the digest queue)
 //   tools/bench_receiver files    <dir> <threads> <files_per_thread> <file_bytes>   (no hashing:
 //                                 the file-system side of the receiver alone)
 //   tools/bench_receiver copy     <dir> <threads> <uploads_per_thread> <upload_bytes>  (no hashing:
-//                                 saveFile's io.Copy(f, body) alone -- 32 KiB socket reads into a
-//                                 user buffer, write, fsync, close: the receiver's host ceiling)
+//                                 saveFile without the digests -- createFile with its .info, open,
+//                                 io.Copy(f, body) in 32 KiB socket reads, fsync, close, the .info
+//                                 removed: the receiver's host ceiling for the same PATCH)
 //
 // Every upload carries the same bytes, so every finished upload must report the digests of a
 // reference upload made before the clock starts; each file is removed when its upload is done
@@ -93,12 +100,42 @@ Response upload(FileReceiver& fr, const std::string& path, const std::vector<uin
   return w;
 }
 
+// The destination server of a drain, without its storage: takes each PATCH body (the socket
+// reads of the real transport), acknowledges the offset, and on the last PATCH answers the SHA-1
+// the content must have (known from a reference read) -- so only the source side's hashing is timed.
+struct SinkTransport : Transport {
+  std::string sha1_hex;
+  Response RoundTrip(const Request& r, Error* err) override {
+    *err = Error{};
+    Response w;
+    if (r.Method == "HEAD") {  // no broken PATCHes here: the sink always has what was sent
+      w.Headers["efes-file-offset"] = "0";
+      return w;
+    }
+    int64_t off = 0, len = -1;
+    (void)ParseInt(r.Headers.count("efes-file-offset") ? r.Headers.at("efes-file-offset") : "0", &off);
+    if (r.Headers.count("efes-file-length")) (void)ParseInt(r.Headers.at("efes-file-length"), &len);
+    uint8_t buf[32 << 10];
+    int64_t n = 0;
+    for (Error e; r.Body;) {
+      n += (int64_t)r.Body->Read(buf, sizeof buf, &e);
+      if (e) break;
+    }
+    if (off + n == len) {
+      w.Headers["efes-file-sha1"] = sha1_hex;
+      w.Headers["efes-file-crc32"] = "00000000";  // sendFile passes it through unchecked (write.go:112)
+    }
+    w.Headers["efes-file-offset"] = std::to_string(off + n);
+    return w;
+  }
+};
+
 }  // namespace
 
 int main(int argc, char** argv) {
   const int pinned_cpus = pin_to_cpu_quota();  // see cpu_quota.hpp
   if (argc < 7 && !(argc >= 6 && (std::string(argv[1]) == "sha1file" || std::string(argv[1]) == "files" ||
-                                  std::string(argv[1]) == "copy"))) {
+                                  std::string(argv[1]) == "copy" || std::string(argv[1]) == "drain"))) {
     fprintf(stderr,
             "usage: %s receiver <dir> <threads> <uploads_per_thread> <upload_bytes> <patch_bytes>\n"
             "       %s sha1file <dir> <threads> <files_per_thread> <file_bytes>\n",
@@ -151,6 +188,9 @@ int main(int argc, char** argv) {
       }
       (void)deleteFile(JoinPath(dir, "/bench/reference.fid"));
     }
+    const char* ph = getenv("EFES_RECEIVER_PHASES");
+    const bool phases = ph && *ph == '1';
+    EnableSavePhases(phases);
     auto t0 = std::chrono::steady_clock::now();
     std::vector<std::thread> th;
     for (int t = 0; t < T; ++t)
@@ -169,13 +209,26 @@ int main(int argc, char** argv) {
       });
     for (auto& x : th) x.join();
     secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    std::string phase_json;
+    if (phases) {  // thread-time per phase, as a share of all request threads' wall time
+      uint64_t ns[kPhases];
+      SavePhaseTotals(ns);
+      phase_json = ", \"phase_share_of_thread_time\": {";
+      for (int p = 0; p < kPhases; ++p) {
+        char b[96];
+        snprintf(b, sizeof b, "%s\"%s\": %.4f", p ? ", " : "", SavePhaseName(p), ns[p] * 1e-9 / (secs * T));
+        phase_json += b;
+      }
+      phase_json += "}";
+      EnableSavePhases(false);
+    }
     delete h;
     for (size_t g = 1; g < ctxs.size(); ++g) efes_ctx_destroy(ctxs[g]);
     printf("{\"workload\": \"receiver\", \"pinned_cpus\": %d, \"gpus\": %d, \"staging_chunks\": %u, \"threads\": %d, \"uploads\": %ld, \"upload_bytes\": %zu, \"patch_bytes\": %zu, "
            "\"read_bytes\": 32768, \"dir_fs\": \"%s\", \"seconds\": %.4f, \"value\": %.3f, \"unit\": \"GiB/s\", "
-           "\"sum_sha1_crc32\": \"%s\", \"all_sums_equal\": %s, \"errors\": %d}\n",
+           "\"sum_sha1_crc32\": \"%s\", \"all_sums_equal\": %s, \"errors\": %d%s}\n",
            pinned_cpus, G, per * (uint32_t)T + 64, T, T * U, S, P, fs_name(dir), secs, (double)T * U * S / secs / (1u << 30), first.c_str(),
-           bad ? "false" : "true", errs.load());
+           bad ? "false" : "true", errs.load(), phase_json.c_str());
   } else if (mode == "files") {
     // The file-system side of the receiver alone (no hashing): per upload, create + 32 KiB
     // writes + fsync + close + unlink, T threads -- the ceiling the receiver can reach here.
@@ -208,8 +261,11 @@ int main(int argc, char** argv) {
            "\"seconds\": %.4f, \"value\": %.3f, \"unit\": \"GiB/s\", \"errors\": %d}\n",
            pinned_cpus, T, T * U, S, fs_name(dir), secs, (double)T * U * S / secs / (1u << 30), errs.load());
   } else if (mode == "copy") {
-    // saveFile without the digests (filereceiver.go:208-223 with MultiWriter(f) only): per upload,
-    // open, io.Copy from the body (32 KiB reads into a buffer, one write each), fsync, close.
+    // saveFile without the digests (filereceiver.go:171-224 with MultiWriter(f) only), the file
+    // work of the receiver's single-PATCH upload exactly: createFile (os.Create + Close + the
+    // newFileInfo .info, :148-165 -- a PATCH at offset 0 makes it, :173-178), OpenFile(O_WRONLY),
+    // io.Copy from the body (32 KiB reads into a buffer, one write each), fsync, close, and
+    // DeleteFileInfo once offset == length (:220-223).
     auto t0 = std::chrono::steady_clock::now();
     std::vector<std::thread> th;
     for (int t = 0; t < T; ++t)
@@ -222,7 +278,11 @@ int main(int argc, char** argv) {
         std::vector<uint8_t> buf(32 << 10);
         for (long u = 0; u < U; ++u) {
           const std::string path = d + "/" + std::to_string(u) + ".fid";
-          const int fd = ::open(path.c_str(), O_RDWR | O_CREAT | O_TRUNC | O_CLOEXEC, 0666);
+          if (createFile(path)) {
+            ++errs;
+            return;
+          }
+          const int fd = ::open(path.c_str(), O_WRONLY | O_CLOEXEC);
           if (fd < 0) {
             ++errs;
             return;
@@ -235,6 +295,7 @@ int main(int argc, char** argv) {
             if (e) break;
           }
           if (::fsync(fd) != 0 || ::close(fd) != 0) ++errs;
+          if (DeleteFileInfo(path)) ++errs;
           unlink(path.c_str());
         }
       });
@@ -292,6 +353,61 @@ int main(int argc, char** argv) {
            "\"all_sums_equal\": %s, \"errors\": %d}\n",
            pinned_cpus, T, T * U, S, fs_name(dir), secs, (double)T * U * S / secs / (1u << 30), first.c_str(), bad ? "false" : "true",
            errs.load());
+  } else if (mode == "drain") {
+    // Files 0..U-1 (written by the caller) moved by T workers, each taking the next fid.
+    const long F = U, NF = argc > 6 ? std::max(1L, atol(argv[6])) : U;
+    auto fid_path = [&](long i) { return dir + "/" + std::to_string(i % NF) + ".fid"; };
+    SinkTransport sink;
+    {  // the content's SHA-1 from one reference read (bench.py checks it against hashlib)
+      FileReader* fr = nullptr;
+      Sha1File* sf = nullptr;
+      if (FileReader::Open(fid_path(0), &fr) || Sha1File::New(fr, ctx, &sf)) {
+        fprintf(stderr, "cannot open %s\n", fid_path(0).c_str());
+        return 1;
+      }
+      std::vector<uint8_t> buf(32 << 10);
+      Error e;
+      while (!e) sf->Read(buf.data(), buf.size(), &e);
+      uint8_t d[20];
+      if (e.code != ERR_EOF || sf->Sum(d)) {
+        fprintf(stderr, "reference read failed\n");
+        return 1;
+      }
+      sink.sha1_hex = first = HexEncode(d, 20);
+      delete sf;
+      delete fr;
+    }
+    ClientConfig cfg;
+    cfg.Drainer = true;  // efes-drain: true (write.go:163-165)
+    std::atomic<long> next{0};
+    auto t0 = std::chrono::steady_clock::now();
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t)
+      th.emplace_back([&] {
+        for (long i; (i = next++) < F;) {  // drain.go:87-101, one fid after the other per worker
+          FileReader* fr = nullptr;
+          if (FileReader::Open(fid_path(i), &fr)) {
+            ++errs;
+            continue;
+          }
+          Checksums cs;
+          Error e = sendFile(sink, ctx, "/drain/" + std::to_string(i) + ".fid", *fr, (int64_t)S, cfg, &cs);
+          if (e) {
+            ++errs;
+            fprintf(stderr, "fid %ld: %s\n", i, e.msg.c_str());
+          } else if (cs.Sha1 != first) {
+            ++bad;
+          }
+          delete fr;
+        }
+      });
+    for (auto& x : th) x.join();
+    secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    printf("{\"workload\": \"drain\", \"pinned_cpus\": %d, \"workers\": %d, \"files\": %ld, \"file_bytes\": %zu, "
+           "\"read_bytes\": 32768, \"dir_fs\": \"%s\", \"seconds\": %.4f, \"value\": %.3f, \"unit\": \"GiB/s\", "
+           "\"sum_sha1\": \"%s\", \"all_sums_equal\": %s, \"errors\": %d}\n",
+           pinned_cpus, T, F, S, fs_name(dir), secs, (double)F * S / secs / (1u << 30), first.c_str(),
+           bad ? "false" : "true", errs.load());
   } else {
     fprintf(stderr, "unknown mode %s\n", mode.c_str());
     return 2;

@@ -74,7 +74,10 @@ def parse_args(argv=None):
     p.add_argument("--ingest-tib", type=float, default=10.0)
     p.add_argument("--ingest-scale", type=float, default=1.0)
     p.add_argument("--ingest-batch", type=int, default=196608,
-                   help="chunks per launch: 3 WIDE waves per SIMD (134 VGPRs -> 3 resident) x 1024 SIMDs x 64")
+                   help="chunks per launch: 3 WIDE waves per SIMD (132 VGPRs -> 3 resident) x 1024 SIMDs x 64")
+    p.add_argument("--ingest-segment", type=int, default=1 << 20,
+                   help="ingest: each 4 MiB chunk as Writes of this many bytes, distinct data in every launch "
+                        "(0: whole chunks aliasing a --pool-gib pool, the round-1/2 leg)")
     p.add_argument("--sha1-only", action="store_true", help="BASELINE configs[1] (no CRC-32)")
     p.add_argument("--cpu-threads", type=int, default=0, help="cpu_baseline threads (0 = host share, max 16)")
     p.add_argument("--cpu-max-chunks", type=int, default=1024)
@@ -274,20 +277,23 @@ def receiver_leg():
         # them beside this process's own runtime threads crossed it once (under rocprof); 768
         # leaves ~200 for the runtimes (12.0-19.0 GiB/s at 1024 threads, 12.7-13.1 at 512).
         # Receiver and copy ceiling alternate, three times: the fraction is the median of the pairs.
-        recv, copy, fracs, ok = [], [], [], True
+        recv, copy, copy_res, fracs, ok = [], [], [], [], True
         want = hashlib.sha1(src).hexdigest() + "%08x" % zlib.crc32(src)
         for _ in range(3):
             r = run(["receiver", d, "768", "4", str(4 << 20), str(4 << 20)])
             ok = ok and r.pop("sum_sha1_crc32") == want and r.pop("all_sums_equal")
             c = run(["copy", d, "768", "4", str(4 << 20)])
             recv.append(r)
+            copy_res.append(c)
             copy.append(c["value"])
             fracs.append(r["value"] / c["value"])
         res = dict(recv[0])
         res.update({"value": round(statistics.median(x["value"] for x in recv), 3),
                     "values": [x["value"] for x in recv], "copy_ceiling": round(statistics.median(copy), 3),
                     "copy_values": copy, "frac_of_copy": round(statistics.median(fracs), 3),
-                    "frac_of_copy_each": [round(f, 3) for f in fracs], "digests_match": bool(ok)})
+                    "frac_of_copy_each": [round(f, 3) for f in fracs], "digests_match": bool(ok),
+                    "cpu_s_per_gib": [x.get("cpu_s_per_gib") for x in recv],
+                    "copy_cpu_s_per_gib": [c.get("cpu_s_per_gib") for c in copy_res]})
         # one more receiver run with saveFile's host-time accounting by phase (efes_receiver.cpp)
         ph = run(["receiver", d, "768", "4", str(4 << 20), str(4 << 20)], {"EFES_RECEIVER_PHASES": "1"})
         res["phases"] = {"value": ph["value"], "share_of_thread_time": ph.get("phase_share_of_thread_time")}
@@ -307,7 +313,6 @@ def drain_leg(workers=(1, 16, 64, 256, 512), file_bytes: int = 4 << 20, cpu_thre
     mirror, every read hashed on the GPU (their streams batched by the digest queue), to a sink
     server; against the CPU port -- the oracle's sha1digest over the same files in 32 KiB reads on
     `cpu_threads` host threads.  Reports the K at which the GPU path overtakes the CPU."""
-    import concurrent.futures
     import hashlib
     import subprocess
     import tempfile
@@ -332,28 +337,22 @@ def drain_leg(workers=(1, 16, 64, 256, 512), file_bytes: int = 4 << 20, cpu_thre
             points.append({"workers": k, "fids": fids, "GiB/s": res["value"],
                            "digests_match": res["sum_sha1"] == want and res["all_sums_equal"] and not res["errors"]})
 
-        def cpu_one(i):  # Sha1File's hashing (sha1file.go:23-37) on the CPU port: 32 KiB reads, one Write each
-            h = oracle.Sha1()
-            with open(os.path.join(d, f"{i % nfiles}.fid"), "rb", buffering=0) as f:
-                while True:
-                    b = f.read(32 << 10)
-                    if not b:
-                        break
-                    h.write(b)
-            return h.hexdigest() == want
-
+        # the CPU port: oracle/drain_cpu (sha1digest's generic block restated in C, 32 KiB reads through
+        # Sha1File's Write) on `cpu_threads` pthreads, one file in flight each, over the same files
         oracle.build()
-        n_cpu, t0 = 0, time.perf_counter()
-        ok_cpu = True
-        with concurrent.futures.ThreadPoolExecutor(cpu_threads) as ex:
-            while time.perf_counter() - t0 < 3.0:
-                ok_cpu = all(ex.map(cpu_one, range(n_cpu, n_cpu + 4 * cpu_threads))) and ok_cpu
-                n_cpu += 4 * cpu_threads
-        cpu = n_cpu * file_bytes / (time.perf_counter() - t0) / GiB
+        exe_cpu = os.path.join(ROOT, "oracle", "drain_cpu")
+        fids_cpu = 4096
+        r = subprocess.run([exe_cpu, d, str(cpu_threads), str(fids_cpu), str(file_bytes), str(nfiles)], check=True,
+                           capture_output=True, text=True, timeout=300)
+        cres = json.loads(r.stdout.strip().splitlines()[-1])
+        cpu = cres["value"]
+        ok_cpu = cres["sum_sha1"] == want and cres["all_sums_equal"] and not cres["errors"]
+        n_cpu = fids_cpu
     over = next((p["workers"] for p in points if p["GiB/s"] > cpu), None)
     return {"unit": "GiB/s", "file_bytes": file_bytes, "points": points,
             "cpu_port": {"value": round(cpu, 3), "cores": cpu_threads, "kind": "port", "digests_match": bool(ok_cpu),
-                         "sample": f"{n_cpu} x {file_bytes >> 20} MiB files, oracle sha1digest in 32 KiB reads"},
+                         "sample": f"{n_cpu} x {file_bytes >> 20} MiB files (oracle/drain_cpu: sha1digest in 32 KiB "
+                                   f"reads, one file per thread at a time, {cres['seconds']} s)"},
             "gpu_overtakes_cpu_at_workers": over,
             "note": "sendFile(Sha1File) per file to a sink server (its SHA-1 answer known), K files in flight; "
                     "one stream is one SHA-1 chain (~90 MB/s), so the GPU needs many files in flight; not `value`"}
@@ -391,6 +390,9 @@ def make_workload(args, rank: int, world: int, ctx, device: str, stream):
                 if (n, chunk) == (1024, 4 << 20) else f"{n} x {chunk} B chunks")
         return data, [b], [n * chunk], {"workload": name, "chunks_per_gpu": n, "chunk_bytes": chunk}
     pool = args.pool_gib << 30
+    if args.workload == "ingest" and args.ingest_segment:
+        per_gpu = int(round(args.ingest_tib * (1 << 40) / (4 << 20) / 8 * args.ingest_scale))
+        pool = min(args.ingest_batch, per_gpu) * args.ingest_segment  # distinct bytes for one launch, no aliasing
     data = torch.empty(pool, dtype=torch.uint8, device=device)
     ctx.fill_synthetic(data.data_ptr(), pool, seed, stream.cuda_stream)
     if args.workload == "mixed":
@@ -406,6 +408,29 @@ def make_workload(args, rank: int, world: int, ctx, device: str, stream):
             "chunks_per_gpu": args.mixed_chunks, "bytes_per_gpu": total, "pool_bytes": pool, "launches": L}
     chunk = 4 << 20
     per_gpu = int(round(args.ingest_tib * (1 << 40) / chunk / 8 * args.ingest_scale))
+    if args.ingest_segment:
+        # Distinct data in every launch: 196 608 x 4 MiB cannot be resident at once (768 GiB), so each
+        # chunk arrives as 4 MiB / segment Writes -- the per-PATCH resume of filereceiver.go:182-226,
+        # as efes_hash_host streams host chunks -- with the states resident in HBM between launches.
+        # Launch (g, s) hashes segment s of the chunks of group g from a buffer of
+        # ingest_batch x segment distinct bytes (re-filled by the "network" between segments in a
+        # real ingest; here the same bytes, so chunk j is its 1 MiB repeated), one job per chunk.
+        seg = args.ingest_segment
+        nseg = chunk // seg
+        batches, nbytes = [], []
+        for start in range(0, per_gpu, args.ingest_batch):
+            m = min(args.ingest_batch, per_gpu - start)
+            base = DeviceBatch(data.data_ptr(), np.arange(m, dtype=np.uint64) * np.uint64(seg), np.full(m, seg),
+                               **dict(kw, fresh=False))
+            for k in range(nseg):
+                batches.append(base.variant(fresh=k == 0, finalize=k == nseg - 1))
+                nbytes.append(m * seg)
+        return data, batches, nbytes, {
+            "workload": f"{args.ingest_tib:g} TiB ingest over 8 GPUs, this GPU's share x{args.ingest_scale:g} "
+                        f"(BASELINE configs[4]): 4 MiB chunks as {nseg} x {seg >> 20} MiB segment Writes, distinct "
+                        f"bytes in every launch",
+            "chunks_per_gpu": per_gpu, "chunk_bytes": chunk, "segment_bytes": seg, "launches": len(batches),
+            "distinct_bytes_per_launch": min(args.ingest_batch, per_gpu) * seg}
     slots = pool // chunk
     batches, nbytes = [], []
     for start in range(0, per_gpu, args.ingest_batch):
@@ -414,7 +439,8 @@ def make_workload(args, rank: int, world: int, ctx, device: str, stream):
         batches.append(DeviceBatch(data.data_ptr(), idx * np.uint64(chunk), np.full(m, chunk), **kw))
         nbytes.append(m * chunk)
     return data, batches, nbytes, {"workload": f"{args.ingest_tib:g} TiB ingest over 8 GPUs, this GPU's share "
-                                               f"x{args.ingest_scale:g} (BASELINE configs[4])",
+                                               f"x{args.ingest_scale:g} (BASELINE configs[4]), chunks aliasing a "
+                                               f"{args.pool_gib} GiB pool",
                                    "chunks_per_gpu": per_gpu, "chunk_bytes": chunk, "pool_bytes": pool,
                                    "launches": len(batches)}
 
@@ -496,6 +522,7 @@ def ingest_leg(args, rank: int, world: int, ctx, device: str, stream, mode: int,
     with torch.cuda.stream(stream):
         data, batches, step_bytes, config = make_workload(a, rank, world, ctx, device, stream)
         wall, kernel_ms = run_timed(batches, len(batches), 1, mode, device, stream, dist)
+        ok = ingest_spot_check(data, batches, config)
     from efes_amd.shard import max_over_ranks
 
     wall = max_over_ranks(wall, device if args.dist_backend == "nccl" else None)
@@ -506,7 +533,7 @@ def ingest_leg(args, rank: int, world: int, ctx, device: str, stream, mode: int,
     del data, batches
     torch.cuda.empty_cache()
     return {"value": round(world * total / wall / GiB, 3), "unit": "GiB/s", "n_gpus": world,
-            "scaling": "weak", "bytes_per_gpu": total, "max_rank_wall_s": round(wall, 4),
+            "scaling": "weak", "bytes_per_gpu": total, "max_rank_wall_s": round(wall, 4), "digests_spot_check": ok,
             "workload": config["workload"],
             "chunks": config["chunks_per_gpu"], "launches": config["launches"], "kernel": "wide_kernel",
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
@@ -544,6 +571,28 @@ def sha1_only_leg(args, ctx, data, fused, device: str, stream):
             "binding_roofline": binding_roofline(kernel, achieved, n, True) if kernel in ("deep_kernel", "wide_kernel")
             else None,
             "digests_match_fused_sha1": ok, "note": "same chunks as the metric, SHA-1 only; not `value`"}
+
+
+def ingest_spot_check(data, batches, config) -> bool:
+    """hashlib/zlib of two chunks per launch group against the Sums of the segmented ingest (chunk j
+    of a group = its segment's bytes, once per segment); True when the leg is not segmented."""
+    import hashlib
+    import zlib
+
+    seg = config.get("segment_bytes")
+    if not seg:
+        return True
+    nseg = config["chunk_bytes"] // seg
+    ok = True
+    for g in range(0, len(batches), nseg):
+        last = batches[g + nseg - 1]
+        for j in (0, last.n - 1):
+            piece = data[j * seg:(j + 1) * seg].cpu().numpy().tobytes()
+            chunk = piece * nseg
+            s = last.sums_host()[j]
+            ok = ok and bytes(s[:20]) == hashlib.sha1(chunk).digest() and \
+                int.from_bytes(bytes(s[20:24]), "big") == zlib.crc32(chunk)
+    return bool(ok)
 
 
 def concurrency_leg(args, ctx, device: str, stream):

@@ -73,6 +73,27 @@ class DeviceBatch:
         self.jobs = torch.from_numpy(jobs.view(np.uint8).copy()).to(device)
         torch.cuda.synchronize(device)
 
+    def variant(self, *, fresh: bool, finalize: bool) -> "DeviceBatch":
+        """The same jobs over the same data, states, sums and status with other flags: one segment
+        of a resumed Write sequence (EFES_JOB_INIT on the first segment, EFES_JOB_FINALIZE on the
+        last; the states stay in HBM between them, filereceiver.go:182-226)."""
+        import copy
+
+        v = copy.copy(self)
+        jobs = self.jobs_host.copy()
+        jobs["flags"] &= np.uint32(~(EFES_JOB_INIT | EFES_JOB_FINALIZE) & 0xFFFFFFFF)
+        if fresh:
+            jobs["flags"] |= EFES_JOB_INIT
+        if finalize:
+            assert int(self.jobs_host["sum"][0]) != 0, "a finalizing variant needs a batch made with finalize=True"
+            jobs["flags"] |= EFES_JOB_FINALIZE
+        v.jobs_host = jobs
+        v.jobs = self.torch.from_numpy(jobs.view(np.uint8).copy()).to(self.device)
+        if hasattr(v, "plan"):
+            del v.plan
+        self.torch.cuda.synchronize(self.device)
+        return v
+
     def stream(self) -> int:
         return self.torch.cuda.current_stream(self.device).cuda_stream
 

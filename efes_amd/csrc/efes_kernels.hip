@@ -1273,35 +1273,14 @@ __device__ __forceinline__ void wide_step(const uint32_t (&le)[16], const uint32
 //    load a harmless `dummy` block and do not commit.
 // kSha/kCrc are wave-uniform template flags; a lane that needs only one of the two computes
 // both and never stores the other.  Jobs sorted by length keep the lanes of a wave equally long.
-// Fair issue among the WIDE waves that share a SIMD.  The SIMD issues from the oldest ready wave
-// first, so of `fair` co-resident waves (all with equally long messages) the oldest runs at nearly
-// its lone-wave rate and ends first, the youngest last -- and alone: a lone WIDE wave issues one
-// VALU per ~5.1 cycles instead of the saturated 4 (its chains' dependencies), so the SIMD idles
-// through that tail (PMC of a configs[4] launch, profiles/r03_wide_pmc: waves alive 65 % of the
-// launch on average, VALU busy 87 %).  Rotating the wave priorities on a shared clock gives every
-// co-resident wave the top priority for an equal share of the time, so they advance together and
-// end together.  slot = the wave's hardware slot on its SIMD, fair = waves per SIMD of the launch.
-constexpr int kWideFairShift = 15;  // priority phase = 2^15 shader clocks (~14 us, ~9 top-priority blocks)
-__device__ __forceinline__ uint32_t wave_slot() {
-  uint32_t v;
-  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID, 0, 4)" : "=s"(v));  // WAVE_ID of HW_ID
-  return v;
-}
-__device__ __forceinline__ void wide_fair_prio(uint32_t fair, uint32_t slot) {
-  if (fair < 2) return;
-  __builtin_amdgcn_sched_barrier(0);
-  const uint32_t ph = ((uint32_t)(__builtin_amdgcn_s_memtime() >> kWideFairShift) + slot) % fair;
-  if (ph == 0) __builtin_amdgcn_s_setprio(3);
-  else if (ph == 1) __builtin_amdgcn_s_setprio(2);
-  else if (ph == 2) __builtin_amdgcn_s_setprio(1);
-  else __builtin_amdgcn_s_setprio(0);
-  __builtin_amdgcn_sched_barrier(0);
-}
-
+#ifndef EFES_WIDE_DEPTH
+#define EFES_WIDE_DEPTH 3
+#endif
+#if EFES_WIDE_DEPTH == 3
 template <bool kAligned16, bool kSha, bool kCrc>
 __device__ __forceinline__ void wide_bulk(const uint8_t* q, uint64_t nbulk, uint64_t nmin, uint64_t nmax,
                                           const uint8_t* dummy, const uint32_t (&t)[8][256], uint32_t (&h)[5],
-                                          uint32_t& crc_raw, uint32_t fair, uint32_t slot) {
+                                          uint32_t& crc_raw) {
   auto src = [&](uint64_t b) { return b < nbulk ? q + 64 * b : dummy; };
   uint32_t A[16], B[16], C[16];
   if (nmax == 0) return;
@@ -1309,7 +1288,6 @@ __device__ __forceinline__ void wide_bulk(const uint8_t* q, uint64_t nbulk, uint
   load_block_le<kAligned16>(src(1), B);
   uint64_t b = 0;
   for (; b + 4 < nmin; b += 3) {  // uniform phase: blocks b..b+4 exist in every lane
-    wide_fair_prio(fair, slot);
     const uint8_t* qb = q + 64 * b;
     load_block_le<kAligned16>(qb + 128, C);
     wide_step<kSha, kCrc>(A, t, h, crc_raw, true);
@@ -1319,7 +1297,6 @@ __device__ __forceinline__ void wide_bulk(const uint8_t* q, uint64_t nbulk, uint
     wide_step<kSha, kCrc>(C, t, h, crc_raw, true);
   }
   for (; b < nmax; b += 3) {  // ragged phase (A, B hold blocks b, b+1 or the dummy)
-    wide_fair_prio(fair, slot);
     load_block_le<kAligned16>(src(b + 2), C);
     wide_step<kSha, kCrc>(A, t, h, crc_raw, b < nbulk);
     if (b + 1 >= nmax) break;
@@ -1330,14 +1307,53 @@ __device__ __forceinline__ void wide_bulk(const uint8_t* q, uint64_t nbulk, uint
     wide_step<kSha, kCrc>(C, t, h, crc_raw, b + 2 < nbulk);
   }
 }
+#else
+// Three blocks in flight per lane (four 16-word buffers, loop unrolled by four): for distinct data
+// in HBM, where the lanes' scattered 64-B reads (each from its own DRAM row) take longer.
+template <bool kAligned16, bool kSha, bool kCrc>
+__device__ __forceinline__ void wide_bulk(const uint8_t* q, uint64_t nbulk, uint64_t nmin, uint64_t nmax,
+                                          const uint8_t* dummy, const uint32_t (&t)[8][256], uint32_t (&h)[5],
+                                          uint32_t& crc_raw) {
+  auto src = [&](uint64_t b) { return b < nbulk ? q + 64 * b : dummy; };
+  uint32_t A[16], B[16], C[16], D[16];
+  if (nmax == 0) return;
+  load_block_le<kAligned16>(src(0), A);
+  load_block_le<kAligned16>(src(1), B);
+  load_block_le<kAligned16>(src(2), C);
+  uint64_t b = 0;
+  for (; b + 6 < nmin; b += 4) {  // uniform phase: blocks b..b+6 exist in every lane
+    const uint8_t* qb = q + 64 * b;
+    load_block_le<kAligned16>(qb + 192, D);
+    wide_step<kSha, kCrc>(A, t, h, crc_raw, true);
+    load_block_le<kAligned16>(qb + 256, A);
+    wide_step<kSha, kCrc>(B, t, h, crc_raw, true);
+    load_block_le<kAligned16>(qb + 320, B);
+    wide_step<kSha, kCrc>(C, t, h, crc_raw, true);
+    load_block_le<kAligned16>(qb + 384, C);
+    wide_step<kSha, kCrc>(D, t, h, crc_raw, true);
+  }
+  for (; b < nmax; b += 4) {  // ragged phase (A, B, C hold blocks b..b+2 or the dummy)
+    load_block_le<kAligned16>(src(b + 3), D);
+    wide_step<kSha, kCrc>(A, t, h, crc_raw, b < nbulk);
+    if (b + 1 >= nmax) break;
+    load_block_le<kAligned16>(src(b + 4), A);
+    wide_step<kSha, kCrc>(B, t, h, crc_raw, b + 1 < nbulk);
+    if (b + 2 >= nmax) break;
+    load_block_le<kAligned16>(src(b + 5), B);
+    wide_step<kSha, kCrc>(C, t, h, crc_raw, b + 2 < nbulk);
+    if (b + 3 >= nmax) break;
+    load_block_le<kAligned16>(src(b + 6), C);
+    wide_step<kSha, kCrc>(D, t, h, crc_raw, b + 3 < nbulk);
+  }
+}
+#endif
 template <bool kAligned16>
 __device__ __forceinline__ void wide_bulk_any(const uint8_t* q, uint64_t nbulk, uint64_t nmin, uint64_t nmax,
                                               const uint8_t* dummy, bool any_sha, bool any_crc,
-                                              const uint32_t (&t)[8][256], uint32_t (&h)[5], uint32_t& crc_raw,
-                                              uint32_t fair, uint32_t slot) {
-  if (any_sha && any_crc) wide_bulk<kAligned16, true, true>(q, nbulk, nmin, nmax, dummy, t, h, crc_raw, fair, slot);
-  else if (any_sha) wide_bulk<kAligned16, true, false>(q, nbulk, nmin, nmax, dummy, t, h, crc_raw, fair, slot);
-  else if (any_crc) wide_bulk<kAligned16, false, true>(q, nbulk, nmin, nmax, dummy, t, h, crc_raw, fair, slot);
+                                              const uint32_t (&t)[8][256], uint32_t (&h)[5], uint32_t& crc_raw) {
+  if (any_sha && any_crc) wide_bulk<kAligned16, true, true>(q, nbulk, nmin, nmax, dummy, t, h, crc_raw);
+  else if (any_sha) wide_bulk<kAligned16, true, false>(q, nbulk, nmin, nmax, dummy, t, h, crc_raw);
+  else if (any_crc) wide_bulk<kAligned16, false, true>(q, nbulk, nmin, nmax, dummy, t, h, crc_raw);
 }
 
 // Wave-wide minimum of a per-lane 64-bit value over the lanes where `use` holds (uniform
@@ -1365,13 +1381,14 @@ __device__ __forceinline__ uint64_t wave_max64(uint64_t v) {
 #ifdef EFES_WIDE_STATS
 // Diagnostic build (tools/wide_stats.py): per wave of the last launch, s_memtime at entry, after
 // the bulk loop and at exit, HW_ID and XCC_ID -- the timeline of the waves sharing each SIMD.
-__device__ unsigned long long g_wide_stats[8192 * 5];
+__device__ unsigned long long g_wide_stats[8192 * 6];
 #endif
 
-__global__ __launch_bounds__(64 * kWideWaves, 2) void wide_kernel(const efes_job* __restrict__ jobs, uint32_t njobs,
-                                                                  const Tables* __restrict__ tabs, uint32_t fair) {
+__global__ __launch_bounds__(64 * kWideWaves, EFES_WIDE_DEPTH == 3 ? 2 : 3) void wide_kernel(const efes_job* __restrict__ jobs, uint32_t njobs,
+                                                                  const Tables* __restrict__ tabs) {
 #ifdef EFES_WIDE_STATS
   const unsigned long long st_t0 = __builtin_amdgcn_s_memtime();
+  const unsigned long long st_r0 = __builtin_amdgcn_s_memrealtime();
 #endif
   __shared__ __attribute__((aligned(16))) WideLDS L;
   {
@@ -1445,9 +1462,8 @@ __global__ __launch_bounds__(64 * kWideWaves, 2) void wide_kernel(const efes_job
   // the shortest message over ALL lanes (a lane without a job has nbulk 0: no uniform phase)
   const uint64_t nmin = wave_min64(nbulk, true);
   const uint8_t* dummy = reinterpret_cast<const uint8_t*>(tabs);  // 36 KiB of valid device memory
-  const uint32_t slot = wave_slot();
-  if (all16) wide_bulk_any<true>(q, nbulk, nmin, nmax, dummy, any_sha, any_crc, L.slice8, h, crc_raw, fair, slot);
-  else wide_bulk_any<false>(q, nbulk, nmin, nmax, dummy, any_sha, any_crc, L.slice8, h, crc_raw, fair, slot);
+  if (all16) wide_bulk_any<true>(q, nbulk, nmin, nmax, dummy, any_sha, any_crc, L.slice8, h, crc_raw);
+  else wide_bulk_any<false>(q, nbulk, nmin, nmax, dummy, any_sha, any_crc, L.slice8, h, crc_raw);
 #ifdef EFES_WIDE_STATS
   const unsigned long long st_t1 = __builtin_amdgcn_s_memtime();
 #endif
@@ -1518,8 +1534,9 @@ __global__ __launch_bounds__(64 * kWideWaves, 2) void wide_kernel(const efes_job
     uint32_t hw, xcc;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    unsigned long long* o = g_wide_stats + 5 * gw;
-    o[0] = st_t0; o[1] = st_t1; o[2] = st_t2; o[3] = hw; o[4] = xcc;
+    const unsigned long long st_r2 = __builtin_amdgcn_s_memrealtime();
+    unsigned long long* o = g_wide_stats + 6 * gw;
+    o[0] = st_t0; o[1] = st_t1; o[2] = st_t2; o[3] = hw; o[4] = xcc; o[5] = (st_r2 - st_r0) << 32 | (st_r0 & 0xffffffffull);
   }
 #endif
 }
@@ -1614,15 +1631,8 @@ hipError_t launch_wide(const efes_job* jobs, uint32_t njobs, const Tables* tabs,
                        int cus) {
   if (njobs == 0) return hipSuccess;
   const uint32_t per = 64 * kWideWaves;
-  // waves per SIMD of this launch (at most the 3 that fit, 132 VGPRs): the priority rotation's period
-  const uint64_t waves = (njobs + 63) / 64, simds = 4ull * (uint64_t)(cus > 0 ? cus : 256);
-  uint32_t fair = exclusive ? 1u : (uint32_t)std::min<uint64_t>(3, (waves + simds - 1) / simds);
-  static const bool off = [] {
-    const char* e = getenv("EFES_WIDE_FAIR");  // A/B switch: 0 = the hardware's oldest-first order
-    return e && !strcmp(e, "0");
-  }();
-  if (off) fair = 1;
-  return launch_reserving(wide_kernel, dim3((njobs + per - 1) / per), dim3(per), exclusive, s, jobs, njobs, tabs, fair);
+  (void)cus;
+  return launch_reserving(wide_kernel, dim3((njobs + per - 1) / per), dim3(per), exclusive, s, jobs, njobs, tabs);
 }
 
 #ifdef EFES_FED_STATS

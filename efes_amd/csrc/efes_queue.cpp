@@ -94,6 +94,7 @@ struct efes_queue {
   int fault = EFES_OK;
   uint64_t n_launches = 0, n_jobs = 0, n_bytes = 0;  // efes_queue_get_stats
   uint64_t n_attempts = 0, inject_at = 0;  // test hook: EFES_FAULT_INJECT_LAUNCH=k fails launch k
+  unsigned ev_flags = hipEventDisableTiming;  // + hipEventBlockingSync: the dispatcher sleeps in retire
   std::thread th;
 
   void run();
@@ -186,7 +187,7 @@ void efes_queue::run() {
     int rc = e == hipSuccess ? EFES_OK : EFES_ERR_HIP;
     if (rc == EFES_OK && inject_at && ++n_attempts == inject_at) rc = EFES_ERR_DEVICE_FAULT;  // as a faulted kernel
     if (rc == EFES_OK) rc = efes_hash_submit_mode(ctx, dj, nb, stream, efes::pcie_mode(ctx, nb));
-    if (rc == EFES_OK && hipEventCreateWithFlags(&b.ev, hipEventDisableTiming) != hipSuccess) rc = EFES_ERR_HIP;
+    if (rc == EFES_OK && hipEventCreateWithFlags(&b.ev, ev_flags) != hipSuccess) rc = EFES_ERR_HIP;
     if (rc == EFES_OK && hipEventRecord(b.ev, stream) != hipSuccess) rc = EFES_ERR_HIP;
     lk.lock();
     if (rc != EFES_OK) {
@@ -274,6 +275,9 @@ int efes_queue_create(efes_ctx* ctx, uint64_t chunk_bytes, uint32_t max_chunks, 
   // Test hook (tests/test_gpu_boundary.py): the k-th launch of every queue created while it is set
   // reports a device fault instead of running, as a kernel that faulted would.
   if (const char* fi = getenv("EFES_FAULT_INJECT_LAUNCH")) q->inject_at = strtoull(fi, nullptr, 10);
+  // EFES_QUEUE_SYNC=block: the dispatcher waits for a launch in the kernel driver instead of
+  // polling the event (A/B of the host CPU it costs beside the request threads).
+  if (const char* qs = getenv("EFES_QUEUE_SYNC"); qs && !strcmp(qs, "block")) q->ev_flags |= hipEventBlockingSync;
   DeviceGuard g(ctx->device);
   hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&q->h_slab), q->chunk * max_chunks, hipHostMallocMapped);
   if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void**>(&q->z_slab), q->h_slab, 0);

@@ -29,6 +29,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <fcntl.h>
+#include <sys/resource.h>
 #include <sys/statfs.h>
 #include <unistd.h>
 
@@ -63,6 +64,14 @@ struct SpanReader : Reader {
     return k;
   }
 };
+
+// CPU seconds (user + system) of the whole process so far; *sys gets the system part.
+double cpu_seconds(double* sys = nullptr) {
+  struct rusage ru;
+  getrusage(RUSAGE_SELF, &ru);
+  if (sys) *sys = ru.ru_stime.tv_sec + 1e-6 * ru.ru_stime.tv_usec;
+  return ru.ru_utime.tv_sec + ru.ru_stime.tv_sec + 1e-6 * (ru.ru_utime.tv_usec + ru.ru_stime.tv_usec);
+}
 
 std::vector<uint8_t> content(size_t n) {
   std::vector<uint8_t> v(n);
@@ -191,6 +200,8 @@ int main(int argc, char** argv) {
     const char* ph = getenv("EFES_RECEIVER_PHASES");
     const bool phases = ph && *ph == '1';
     EnableSavePhases(phases);
+    double s0 = 0, s1 = 0;
+    const double c0 = cpu_seconds(&s0);
     auto t0 = std::chrono::steady_clock::now();
     std::vector<std::thread> th;
     for (int t = 0; t < T; ++t)
@@ -209,6 +220,7 @@ int main(int argc, char** argv) {
       });
     for (auto& x : th) x.join();
     secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    const double cpu_s = cpu_seconds(&s1) - c0;
     std::string phase_json;
     if (phases) {  // thread-time per phase, as a share of all request threads' wall time
       uint64_t ns[kPhases];
@@ -226,9 +238,10 @@ int main(int argc, char** argv) {
     for (size_t g = 1; g < ctxs.size(); ++g) efes_ctx_destroy(ctxs[g]);
     printf("{\"workload\": \"receiver\", \"pinned_cpus\": %d, \"gpus\": %d, \"staging_chunks\": %u, \"threads\": %d, \"uploads\": %ld, \"upload_bytes\": %zu, \"patch_bytes\": %zu, "
            "\"read_bytes\": 32768, \"dir_fs\": \"%s\", \"seconds\": %.4f, \"value\": %.3f, \"unit\": \"GiB/s\", "
-           "\"sum_sha1_crc32\": \"%s\", \"all_sums_equal\": %s, \"errors\": %d%s}\n",
+           "\"sum_sha1_crc32\": \"%s\", \"all_sums_equal\": %s, \"errors\": %d, \"cpu_s_per_gib\": %.4f, \"sys_share\": %.3f%s}\n",
            pinned_cpus, G, per * (uint32_t)T + 64, T, T * U, S, P, fs_name(dir), secs, (double)T * U * S / secs / (1u << 30), first.c_str(),
-           bad ? "false" : "true", errs.load(), phase_json.c_str());
+           bad ? "false" : "true", errs.load(), cpu_s / ((double)T * U * S / (1u << 30)), (s1 - s0) / cpu_s,
+           phase_json.c_str());
   } else if (mode == "files") {
     // The file-system side of the receiver alone (no hashing): per upload, create + 32 KiB
     // writes + fsync + close + unlink, T threads -- the ceiling the receiver can reach here.
@@ -266,6 +279,8 @@ int main(int argc, char** argv) {
     // newFileInfo .info, :148-165 -- a PATCH at offset 0 makes it, :173-178), OpenFile(O_WRONLY),
     // io.Copy from the body (32 KiB reads into a buffer, one write each), fsync, close, and
     // DeleteFileInfo once offset == length (:220-223).
+    double s0 = 0, s1 = 0;
+    const double c0 = cpu_seconds(&s0);
     auto t0 = std::chrono::steady_clock::now();
     std::vector<std::thread> th;
     for (int t = 0; t < T; ++t)
@@ -301,9 +316,12 @@ int main(int argc, char** argv) {
       });
     for (auto& x : th) x.join();
     secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    const double cpu_s = cpu_seconds(&s1) - c0;
     printf("{\"workload\": \"copy\", \"pinned_cpus\": %d, \"threads\": %d, \"uploads\": %ld, \"upload_bytes\": %zu, "
-           "\"read_bytes\": 32768, \"dir_fs\": \"%s\", \"seconds\": %.4f, \"value\": %.3f, \"unit\": \"GiB/s\", \"errors\": %d}\n",
-           pinned_cpus, T, T * U, S, fs_name(dir), secs, (double)T * U * S / secs / (1u << 30), errs.load());
+           "\"read_bytes\": 32768, \"dir_fs\": \"%s\", \"seconds\": %.4f, \"value\": %.3f, \"unit\": \"GiB/s\", \"errors\": %d, "
+           "\"cpu_s_per_gib\": %.4f, \"sys_share\": %.3f}\n",
+           pinned_cpus, T, T * U, S, fs_name(dir), secs, (double)T * U * S / secs / (1u << 30), errs.load(),
+           cpu_s / ((double)T * U * S / (1u << 30)), (s1 - s0) / cpu_s);
   } else if (mode == "sha1file") {
     // One source file read by every thread U times through Sha1File (32 KiB reads).
     const std::string path = dir + "/bench_sha1file.dat";

@@ -1,8 +1,9 @@
 #!/bin/bash
 # ThreadSanitizer build of the HOST code (the reference runs `go test -race`): the
 # library's host side (dispatcher, queue, uploads, streaming digests) instrumented with
-# -fsanitize=thread via -Xarch_host (device code untouched), and the uploads harness linked
-# against it.  Outputs (git-ignored): efes_amd/lib/tsan/libefeshash.so, tools/bench_uploads_tsan.
+# -fsanitize=thread via -Xarch_host (device code untouched), and the uploads harness and the C
+# consumer of the digest surface linked against it.  Outputs (git-ignored):
+# efes_amd/lib/tsan/libefeshash.so, tools/bench_uploads_tsan, tests/c/efes_consumer_test_tsan.
 set -e
 cd "$(dirname "$0")/.."
 mkdir -p efes_amd/lib/tsan
@@ -12,3 +13,6 @@ $HIPCC --offload-arch=gfx950 -O1 -g -std=c++17 -fPIC -shared -Xarch_host -fsanit
   efes_amd/csrc/efes_ingest.cpp efes_amd/csrc/efes_queue.cpp efes_amd/csrc/efes_stream.cpp efes_amd/csrc/efes_plan.cpp
 $HIPCC -O1 -g -std=c++17 -fsanitize=thread -I include tools/bench_uploads.cpp -o tools/bench_uploads_tsan \
   -L efes_amd/lib/tsan -lefeshash -Wl,-rpath,'$ORIGIN/../efes_amd/lib/tsan' -pthread
+/opt/rocm/lib/llvm/bin/clang -O1 -g -std=c11 -fsanitize=thread -pthread tests/c/efes_consumer_test.c \
+  -o tests/c/efes_consumer_test_tsan -L efes_amd/lib/tsan -lefeshash -L oracle -loracle \
+  -Wl,-rpath,'$ORIGIN/../../efes_amd/lib/tsan' -Wl,-rpath,'$ORIGIN/../../oracle'

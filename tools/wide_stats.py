@@ -23,7 +23,7 @@ from efes_amd.hashing import default_context  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 196608
 size = int(sys.argv[2]) if len(sys.argv) > 2 else 4 << 20
-pool = 16 << 30
+pool = int(sys.argv[3]) << 30 if len(sys.argv) > 3 else 16 << 30  # GiB; n * size <= pool: no aliasing
 ctx = default_context(0)
 buf = torch.empty(pool, dtype=torch.uint8, device="cuda:0")
 ctx.fill_synthetic(buf.data_ptr(), pool, 1, torch.cuda.current_stream().cuda_stream)
@@ -33,17 +33,21 @@ b.run(MODE_WIDE)  # warm-up
 b.reset()
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 e0.record()
-b.run(MODE_WIDE)
+b.submit(MODE_WIDE)  # two launches back to back (as bench.py's steps): the stats are the second's
+b.submit(MODE_WIDE)
 e1.record()
 torch.cuda.synchronize()
-ms = e0.elapsed_time(e1)
+ms = e0.elapsed_time(e1) / 2
 W = 8192
-out = (ctypes.c_ulonglong * (W * 5))()
+out = (ctypes.c_ulonglong * (W * 6))()
 L = lib()
 L.efes_debug_wide_stats.argtypes = [ctypes.c_void_p]
 assert L.efes_debug_wide_stats(out) == 0
-v = np.frombuffer(out, dtype=np.uint64).reshape(W, 5)[: (n + 63) // 64].astype(np.int64)
-t0, t1, t2, hw, xcc = v.T
+v = np.frombuffer(out, dtype=np.uint64).reshape(W, 6)[: (n + 63) // 64].astype(np.int64)
+t0, t1, t2, hw, xcc, rt = v.T
+r0 = rt & 0xFFFFFFFF  # s_memrealtime (100 MHz, one clock for the whole chip) at entry, and the lifetime
+rlife = rt >> 32
+r0 = (r0 - r0.min()) & 0xFFFFFFFF
 np.save(os.path.join(ROOT, "gpurun_out", f"wide_stats_raw_f{os.environ.get('EFES_WIDE_FAIR', 'd')}.npy"), v)
 # s_memtime counts per XCD with its own offset: times are taken relative to each XCD's first start
 xs = (xcc & 0xF).astype(int)
@@ -73,6 +77,11 @@ res = {
     "bulk_end_rel_pct": [round(float(x), 4) for x in np.percentile(rel(t1), [0, 10, 50, 90, 100])],
     "end_rel_pct": [round(float(x), 4) for x in np.percentile(rel(t2), [0, 10, 50, 90, 100])],
     "mean_lifetime_rel": round(float(np.mean(rel(t2) - rel(t0))), 4),
+    "realtime_start_ms_pct": [round(float(x) / 1e5, 3) for x in np.percentile(r0, [0, 10, 50, 90, 100])],
+    "realtime_end_ms_pct": [round(float(x) / 1e5, 3) for x in np.percentile(r0 + rlife, [0, 10, 50, 90, 100])],
+    "realtime_life_ms_by_slot": {int(sl): [round(float(x) / 1e5, 2) for x in np.percentile(rlife[(hw & 15) == sl],
+                                                                                       [0, 50, 100])]
+                                 for sl in np.unique(hw & 15)},
     "waves_per_simd_histogram": {str(k): c for k, c in sorted(per.items())},
     "mean_end_by_rank_on_simd": {f"{k[0]}w_rank{k[1]}": round(float(np.mean(e)), 4) for k, e in sorted(rank_end.items())},
 }

@@ -296,7 +296,9 @@ def receiver_leg():
                     "copy_cpu_s_per_gib": [c.get("cpu_s_per_gib") for c in copy_res]})
         # one more receiver run with saveFile's host-time accounting by phase (efes_receiver.cpp)
         ph = run(["receiver", d, "768", "4", str(4 << 20), str(4 << 20)], {"EFES_RECEIVER_PHASES": "1"})
-        res["phases"] = {"value": ph["value"], "share_of_thread_time": ph.get("phase_share_of_thread_time")}
+        res["phases"] = {"value": ph["value"], "cpu_s_per_gib": ph.get("cpu_s_per_gib"),
+                         "request_threads_cpu_s_per_gib": ph.get("request_threads_cpu_s_per_gib"),
+                         "phase_cpu_s_per_gib": ph.get("phase_cpu_s_per_gib")}
         out["receiver"] = res
         r = run(["sha1file", d, "256", "4", str(4 << 20)])
         r["digests_match"] = r.pop("sum_sha1") == hashlib.sha1(src).hexdigest() and r.pop("all_sums_equal")

@@ -33,6 +33,8 @@
 #include <thread>
 #include <vector>
 
+#include <emmintrin.h>
+
 #include "efes_internal.hpp"
 
 using efes::DeviceGuard;
@@ -94,7 +96,10 @@ struct efes_queue {
   int fault = EFES_OK;
   uint64_t n_launches = 0, n_jobs = 0, n_bytes = 0;  // efes_queue_get_stats
   uint64_t n_attempts = 0, inject_at = 0;  // test hook: EFES_FAULT_INJECT_LAUNCH=k fails launch k
-  unsigned ev_flags = hipEventDisableTiming;  // + hipEventBlockingSync: the dispatcher sleeps in retire
+  // hipEventBlockingSync: the dispatcher sleeps in retire instead of polling the event, so it does
+  // not keep a host core busy beside the request threads (receiver within noise either way:
+  // profiles/r03_receiver/ab_sync_*.log); EFES_QUEUE_SYNC=spin restores the poll.
+  unsigned ev_flags = hipEventDisableTiming | hipEventBlockingSync;
   std::thread th;
 
   void run();
@@ -246,6 +251,35 @@ void pace(efes_upload* u, std::unique_lock<std::mutex>& lk) {
     u->done.wait(lk, [&] { return q->fault || u->inflight < q->ahead; });
 }
 
+// memcpy into a staging chunk with non-temporal stores: the chunk is read next by the GPU over
+// PCIe, not by this core, so the copy skips the read-for-ownership of every destination line and
+// leaves the caller's cache alone (one DRAM write per byte instead of a read and a write).
+// Ends with sfence: the stores are visible before the chunk is handed to the dispatcher.
+void copy_to_staging(uint8_t* dst, const uint8_t* src, size_t n) {
+  if (n < 4096) {
+    memcpy(dst, src, n);
+    return;
+  }
+  const size_t head = (16 - (reinterpret_cast<uintptr_t>(dst) & 15)) & 15;
+  memcpy(dst, src, head);
+  dst += head;
+  src += head;
+  n -= head;
+  size_t i = 0;
+  for (; i + 64 <= n; i += 64) {
+    const __m128i a = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i));
+    const __m128i b = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 16));
+    const __m128i c = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 32));
+    const __m128i d = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 48));
+    _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i), a);
+    _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 16), b);
+    _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 32), c);
+    _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 48), d);
+  }
+  memcpy(dst + i, src + i, n - i);
+  _mm_sfence();
+}
+
 int wait_idle(efes_upload* u) {
   efes_queue* q = u->q;
   std::unique_lock<std::mutex> lk(q->mu);
@@ -275,9 +309,7 @@ int efes_queue_create(efes_ctx* ctx, uint64_t chunk_bytes, uint32_t max_chunks, 
   // Test hook (tests/test_gpu_boundary.py): the k-th launch of every queue created while it is set
   // reports a device fault instead of running, as a kernel that faulted would.
   if (const char* fi = getenv("EFES_FAULT_INJECT_LAUNCH")) q->inject_at = strtoull(fi, nullptr, 10);
-  // EFES_QUEUE_SYNC=block: the dispatcher waits for a launch in the kernel driver instead of
-  // polling the event (A/B of the host CPU it costs beside the request threads).
-  if (const char* qs = getenv("EFES_QUEUE_SYNC"); qs && !strcmp(qs, "block")) q->ev_flags |= hipEventBlockingSync;
+  if (const char* qs = getenv("EFES_QUEUE_SYNC"); qs && !strcmp(qs, "spin")) q->ev_flags = hipEventDisableTiming;
   DeviceGuard g(ctx->device);
   hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&q->h_slab), q->chunk * max_chunks, hipHostMallocMapped);
   if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void**>(&q->z_slab), q->h_slab, 0);
@@ -414,7 +446,7 @@ int efes_upload_write(efes_upload* u, const void* p, size_t n) {
       u->fill = 0;
     }
     const uint64_t take = std::min<uint64_t>(n, q->chunk - u->fill);
-    memcpy(q->h_slab + (size_t)u->cur * q->chunk + u->fill, src, take);
+    copy_to_staging(q->h_slab + (size_t)u->cur * q->chunk + u->fill, src, take);
     u->fill += take;
     src += take;
     n -= take;

@@ -8,6 +8,7 @@
 #include <stdio.h>
 #include <string.h>
 #include <sys/stat.h>
+#include <time.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -670,15 +671,21 @@ std::atomic<uint64_t> g_phase_ns[kPhases];
 const char* const kPhaseNames[kPhases] = {"create", "open", "reserve", "read", "write", "commit", "sync", "sum",
                                           "info"};
 
-// Charges the time since the last mark to a phase (when enabled).
+// Charges the calling thread's CPU time (user + system) since the last mark to a phase (when
+// enabled): with hundreds of request threads on 16 cores, wall time per phase would mostly be
+// run-queue waits.
+uint64_t thread_cpu_ns() {
+  struct timespec ts;
+  clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
+  return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
 struct PhaseClock {
   bool on = g_phases_on.load(std::memory_order_relaxed);
-  std::chrono::steady_clock::time_point t = on ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point{};
+  uint64_t t = on ? thread_cpu_ns() : 0;
   void mark(SavePhase p) {
     if (!on) return;
-    const auto now = std::chrono::steady_clock::now();
-    g_phase_ns[p].fetch_add((uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(now - t).count(),
-                            std::memory_order_relaxed);
+    const uint64_t now = thread_cpu_ns();
+    g_phase_ns[p].fetch_add(now - t, std::memory_order_relaxed);
     t = now;
   }
 };
@@ -740,7 +747,39 @@ Error saveFile(Hasher* h, const std::string& path, int64_t offset, int64_t lengt
   // written from it, and the commit hashes it in place -- one host copy fewer than a Write.
   constexpr size_t kCopyBuf = 32 << 10;
   int64_t n = 0;
-  for (;;) {
+  // io.Copy's own 32 KiB buffer (cache-hot: the body is read into it and the file written from it),
+  // then one Write into the upload's staging with streaming stores (efes_upload_write): 0.45-0.47
+  // request-thread CPU-s per GiB against 0.56-0.58 for reading the body straight into the pinned
+  // staging (efes_upload_reserve/commit), whose cold lines cost a read-for-ownership each and
+  // then serve the file write from farther away (profiles/r03_receiver/ab_copybuf.log).
+  // EFES_RECEIVER_COPYBUF=0 selects the reserve/commit path.
+  static const bool staged_copy = [] {
+    const char* e = getenv("EFES_RECEIVER_COPYBUF");
+    return !(e && *e == '0');
+  }();
+  if (staged_copy) {
+    static thread_local uint8_t cbuf[kCopyBuf];
+    for (;;) {
+      Error er;
+      const size_t nr = r.Read(cbuf, kCopyBuf, &er);
+      pc.mark(kPhaseRead);
+      if (nr > 0) {
+        size_t nw = 0;
+        Error ew = write_full(f.fd, path, cbuf, nr, &nw);
+        pc.mark(kPhaseWrite);
+        if (ew) {
+          n += (int64_t)nw;
+          break;
+        }
+        rc = efes_upload_write(g.u, cbuf, nr);  // CRC32.Write, Sha1.Write: staged with streaming stores
+        if (rc) return lib_error(rc);
+        pc.mark(kPhaseCommit);
+        n += (int64_t)nr;
+      }
+      if (er) break;
+    }
+  }
+  for (; !staged_copy;) {
     void* sp = nullptr;
     size_t room = 0;
     rc = efes_upload_reserve(g.u, kCopyBuf, &sp, &room);

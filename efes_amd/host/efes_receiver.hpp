@@ -158,9 +158,10 @@ Error saveFile(Hasher* h, const std::string& path, int64_t offset, int64_t lengt
                int64_t* new_offset, bool* done, DigestSums* sums);
 std::string OffsetMismatchText(int64_t given, int64_t required);  // OffsetMismatchError.Error()
 
-// Host-time accounting of saveFile by phase (tools/bench_receiver, EFES_RECEIVER_PHASES=1):
-// nanoseconds summed over every request, per phase.  Off by default (one branch per phase);
-// when on, one steady_clock read and one relaxed atomic add per phase.
+// Host CPU accounting of saveFile by phase (tools/bench_receiver, EFES_RECEIVER_PHASES=1): the
+// request threads' CPU nanoseconds (CLOCK_THREAD_CPUTIME_ID) summed over every request, per
+// phase.  Off by default (one branch per phase); when on, one clock read and one relaxed atomic
+// add per phase.
 enum SavePhase {
   kPhaseCreate,   // createFile: os.Create + Close + the newFileInfo .info (filereceiver.go:148-165)
   kPhaseOpen,     // ReadFileInfo / OpenFile / Seek / upload slot + efes_upload_open

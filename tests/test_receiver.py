@@ -18,10 +18,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 EXE = os.path.join(ROOT, "tests", "cpp", "receiver_test")
 
 
-def _run(args, timeout):
+def _run(args, timeout, env=None):
     if not os.path.exists(EXE):
         pytest.fail(f"{EXE} not built (__graft_entry__.build())")
-    return subprocess.run([EXE] + args, capture_output=True, text=True, timeout=timeout)
+    return subprocess.run([EXE] + args, capture_output=True, text=True, timeout=timeout,
+                          env=dict(os.environ, **(env or {})))
 
 
 def test_receiver_cpu(tmp_path):
@@ -31,10 +32,13 @@ def test_receiver_cpu(tmp_path):
 
 
 @pytest.mark.gpu
-def test_receiver_gpu(tmp_path):
+@pytest.mark.parametrize("copybuf", ["1", "0"], ids=["copybuf", "reserve_commit"])
+def test_receiver_gpu(tmp_path, copybuf):
+    """saveFile's two staging paths: io.Copy's buffer + efes_upload_write (default) and the body read
+    straight into the pinned staging (efes_upload_reserve/commit, EFES_RECEIVER_COPYBUF=0)."""
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    r = _run(["gpu", str(tmp_path), "16", "4"], 110)
+    r = _run(["gpu", str(tmp_path), "16", "4"], 110, {"EFES_RECEIVER_COPYBUF": copybuf})
     assert r.returncode == 0, r.stdout + r.stderr
     assert "receiver_test gpu ok" in r.stdout, r.stdout

@@ -31,6 +31,7 @@
 #include <fcntl.h>
 #include <sys/resource.h>
 #include <sys/statfs.h>
+#include <time.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -71,6 +72,12 @@ double cpu_seconds(double* sys = nullptr) {
   getrusage(RUSAGE_SELF, &ru);
   if (sys) *sys = ru.ru_stime.tv_sec + 1e-6 * ru.ru_stime.tv_usec;
   return ru.ru_utime.tv_sec + ru.ru_stime.tv_sec + 1e-6 * (ru.ru_utime.tv_usec + ru.ru_stime.tv_usec);
+}
+
+uint64_t thread_cpu_ns() {
+  struct timespec ts;
+  clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
+  return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
 }
 
 std::vector<uint8_t> content(size_t n) {
@@ -200,6 +207,7 @@ int main(int argc, char** argv) {
     const char* ph = getenv("EFES_RECEIVER_PHASES");
     const bool phases = ph && *ph == '1';
     EnableSavePhases(phases);
+    std::atomic<uint64_t> req_cpu_ns{0}, unlink_cpu_ns{0};
     double s0 = 0, s1 = 0;
     const double c0 = cpu_seconds(&s0);
     auto t0 = std::chrono::steady_clock::now();
@@ -215,23 +223,32 @@ int main(int argc, char** argv) {
             return;
           }
           if (w.Headers["efes-file-sha1"] + w.Headers["efes-file-crc32"] != first) ++bad;
+          const uint64_t u0 = thread_cpu_ns();
           (void)deleteFile(JoinPath(dir, path));
+          unlink_cpu_ns += thread_cpu_ns() - u0;
         }
+        struct timespec ts;
+        clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
+        req_cpu_ns += (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
       });
     for (auto& x : th) x.join();
     secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     const double cpu_s = cpu_seconds(&s1) - c0;
     std::string phase_json;
-    if (phases) {  // thread-time per phase, as a share of all request threads' wall time
+    if (phases) {  // request-thread CPU seconds per GiB in each saveFile phase (the rest: outside saveFile)
       uint64_t ns[kPhases];
       SavePhaseTotals(ns);
-      phase_json = ", \"phase_share_of_thread_time\": {";
+      const double gib = (double)T * U * S / (1u << 30);
+      phase_json = ", \"phase_cpu_s_per_gib\": {";
       for (int p = 0; p < kPhases; ++p) {
         char b[96];
-        snprintf(b, sizeof b, "%s\"%s\": %.4f", p ? ", " : "", SavePhaseName(p), ns[p] * 1e-9 / (secs * T));
+        snprintf(b, sizeof b, "%s\"%s\": %.4f", p ? ", " : "", SavePhaseName(p), ns[p] * 1e-9 / gib);
         phase_json += b;
       }
-      phase_json += "}";
+      char b[96];
+      snprintf(b, sizeof b, "}, \"request_threads_cpu_s_per_gib\": %.4f, \"unlink_cpu_s_per_gib\": %.4f",
+               req_cpu_ns.load() * 1e-9 / gib, unlink_cpu_ns.load() * 1e-9 / gib);
+      phase_json += b;
       EnableSavePhases(false);
     }
     delete h;
@@ -279,6 +296,7 @@ int main(int argc, char** argv) {
     // newFileInfo .info, :148-165 -- a PATCH at offset 0 makes it, :173-178), OpenFile(O_WRONLY),
     // io.Copy from the body (32 KiB reads into a buffer, one write each), fsync, close, and
     // DeleteFileInfo once offset == length (:220-223).
+    std::atomic<uint64_t> copy_ph[5] = {};
     double s0 = 0, s1 = 0;
     const double c0 = cpu_seconds(&s0);
     auto t0 = std::chrono::steady_clock::now();
@@ -291,12 +309,19 @@ int main(int argc, char** argv) {
           return;
         }
         std::vector<uint8_t> buf(32 << 10);
+        uint64_t ph[5] = {0, 0, 0, 0, 0}, t = thread_cpu_ns();
+        auto mark = [&](int p) {
+          const uint64_t now = thread_cpu_ns();
+          ph[p] += now - t;
+          t = now;
+        };
         for (long u = 0; u < U; ++u) {
           const std::string path = d + "/" + std::to_string(u) + ".fid";
           if (createFile(path)) {
             ++errs;
             return;
           }
+          mark(0);
           const int fd = ::open(path.c_str(), O_WRONLY | O_CLOEXEC);
           if (fd < 0) {
             ++errs;
@@ -309,19 +334,28 @@ int main(int argc, char** argv) {
             if (n && ::write(fd, buf.data(), n) != (ssize_t)n) ++errs;
             if (e) break;
           }
+          mark(1);
           if (::fsync(fd) != 0 || ::close(fd) != 0) ++errs;
+          mark(2);
           if (DeleteFileInfo(path)) ++errs;
+          mark(3);
           unlink(path.c_str());
+          mark(4);
         }
+        for (int p = 0; p < 5; ++p) copy_ph[p] += ph[p];
       });
     for (auto& x : th) x.join();
     secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     const double cpu_s = cpu_seconds(&s1) - c0;
     printf("{\"workload\": \"copy\", \"pinned_cpus\": %d, \"threads\": %d, \"uploads\": %ld, \"upload_bytes\": %zu, "
            "\"read_bytes\": 32768, \"dir_fs\": \"%s\", \"seconds\": %.4f, \"value\": %.3f, \"unit\": \"GiB/s\", \"errors\": %d, "
-           "\"cpu_s_per_gib\": %.4f, \"sys_share\": %.3f}\n",
+           "\"cpu_s_per_gib\": %.4f, \"sys_share\": %.3f, \"phase_cpu_s_per_gib\": {\"create\": %.4f, "
+           "\"read_write\": %.4f, \"sync_close\": %.4f, \"info\": %.4f, \"unlink\": %.4f}}\n",
            pinned_cpus, T, T * U, S, fs_name(dir), secs, (double)T * U * S / secs / (1u << 30), errs.load(),
-           cpu_s / ((double)T * U * S / (1u << 30)), (s1 - s0) / cpu_s);
+           cpu_s / ((double)T * U * S / (1u << 30)), (s1 - s0) / cpu_s,
+           copy_ph[0] * 1e-9 / ((double)T * U * S / (1u << 30)), copy_ph[1] * 1e-9 / ((double)T * U * S / (1u << 30)),
+           copy_ph[2] * 1e-9 / ((double)T * U * S / (1u << 30)), copy_ph[3] * 1e-9 / ((double)T * U * S / (1u << 30)),
+           copy_ph[4] * 1e-9 / ((double)T * U * S / (1u << 30)));
   } else if (mode == "sha1file") {
     // One source file read by every thread U times through Sha1File (32 KiB reads).
     const std::string path = dir + "/bench_sha1file.dat";

@@ -1180,13 +1180,44 @@ __global__ __launch_bounds__(256, 1) void fed_kernel(const efes_job* __restrict_
 // ================================================================== WIDE kernel
 // One lane per job.  Per-lane tail buffers live in LDS with a 68-byte stride (17 dwords:
 // lanes touching the same byte index hit different banks).
-constexpr int kWideWaves = 4;
+//
+// A workgroup holds every wave a SIMD will run in the launch: 4 x wps waves (wps = waves per SIMD,
+// 1..3; wave w runs on SIMD w % 4), one workgroup per CU.  The SIMD issues from the oldest ready
+// wave first, so of wps waves with equally long messages the oldest ran at nearly a lone wave's
+// rate and ended first, and the last one ran alone -- at a lone wave's ~5.1 cycles per VALU
+// instead of 4 -- for the last ~30 % of the launch (per-wave timeline, profiles/r03_wide_timeline:
+// the SIMD busy 62 of 72.5 ms).  So the waves of a SIMD publish their progress in LDS and, once per
+// loop iteration, the furthest behind takes the top priority and the furthest ahead the lowest
+// (s_setprio): they advance together and end together.
+constexpr int kWideWaves = 4;    // waves per workgroup per SIMD-wave (one per SIMD)
+constexpr int kWideMaxWps = 3;   // waves per SIMD that fit (132 VGPRs)
 constexpr int kXStride = 68;
 
 struct WideLDS {
   uint32_t slice8[8][256];
-  uint8_t xs[kWideWaves * 64][kXStride];
+  uint32_t prog[kWideWaves * kWideMaxWps];  // blocks done by each wave of the workgroup
 };
+
+// The priority of wave w from its SIMD siblings' progress (w % 4, w % 4 + 4, ...): the furthest
+// behind gets 3, the furthest ahead 0, the rest 1.  Wave-uniform; `b` = blocks this wave has done.
+__device__ __forceinline__ void wide_pace(uint32_t* prog, uint32_t w, uint32_t nw, uint32_t b) {
+  if (nw <= kWideWaves) return;  // one wave per SIMD: nothing to share
+  __builtin_amdgcn_sched_barrier(0);
+  if ((threadIdx.x & 63) == 0) __atomic_store_n(&prog[w], b, __ATOMIC_RELAXED);
+  uint32_t lo = 0xffffffffu, hi = 0;
+  for (uint32_t v = w & 3; v < nw; v += kWideWaves) {
+    if (v == w) continue;
+    const uint32_t o = __atomic_load_n(&prog[v], __ATOMIC_RELAXED);
+    lo = o < lo ? o : lo;
+    hi = o > hi ? o : hi;
+  }
+  lo = uniform32(lo);
+  hi = uniform32(hi);
+  if (b <= lo) __builtin_amdgcn_s_setprio(3);
+  else if (b >= hi) __builtin_amdgcn_s_setprio(0);
+  else __builtin_amdgcn_s_setprio(1);
+  __builtin_amdgcn_sched_barrier(0);
+}
 
 // Byte i of the padded final stream x[:nxf] || 0x80 || 0.. || BE64(bits), length T.
 __device__ __forceinline__ uint32_t fin_byte(const uint8_t* xl, uint32_t i, uint32_t nxf, uint32_t T, uint64_t bits) {
@@ -1273,14 +1304,10 @@ __device__ __forceinline__ void wide_step(const uint32_t (&le)[16], const uint32
 //    load a harmless `dummy` block and do not commit.
 // kSha/kCrc are wave-uniform template flags; a lane that needs only one of the two computes
 // both and never stores the other.  Jobs sorted by length keep the lanes of a wave equally long.
-#ifndef EFES_WIDE_DEPTH
-#define EFES_WIDE_DEPTH 3
-#endif
-#if EFES_WIDE_DEPTH == 3
 template <bool kAligned16, bool kSha, bool kCrc>
 __device__ __forceinline__ void wide_bulk(const uint8_t* q, uint64_t nbulk, uint64_t nmin, uint64_t nmax,
                                           const uint8_t* dummy, const uint32_t (&t)[8][256], uint32_t (&h)[5],
-                                          uint32_t& crc_raw) {
+                                          uint32_t& crc_raw, uint32_t* prog, uint32_t w, uint32_t nw) {
   auto src = [&](uint64_t b) { return b < nbulk ? q + 64 * b : dummy; };
   uint32_t A[16], B[16], C[16];
   if (nmax == 0) return;
@@ -1288,6 +1315,7 @@ __device__ __forceinline__ void wide_bulk(const uint8_t* q, uint64_t nbulk, uint
   load_block_le<kAligned16>(src(1), B);
   uint64_t b = 0;
   for (; b + 4 < nmin; b += 3) {  // uniform phase: blocks b..b+4 exist in every lane
+    if (b % 6 == 0) wide_pace(prog, w, nw, (uint32_t)b);  // every 6 blocks: ~4 VALU per block
     const uint8_t* qb = q + 64 * b;
     load_block_le<kAligned16>(qb + 128, C);
     wide_step<kSha, kCrc>(A, t, h, crc_raw, true);
@@ -1297,6 +1325,7 @@ __device__ __forceinline__ void wide_bulk(const uint8_t* q, uint64_t nbulk, uint
     wide_step<kSha, kCrc>(C, t, h, crc_raw, true);
   }
   for (; b < nmax; b += 3) {  // ragged phase (A, B hold blocks b, b+1 or the dummy)
+    if (b % 6 == 0) wide_pace(prog, w, nw, (uint32_t)b);
     load_block_le<kAligned16>(src(b + 2), C);
     wide_step<kSha, kCrc>(A, t, h, crc_raw, b < nbulk);
     if (b + 1 >= nmax) break;
@@ -1307,53 +1336,14 @@ __device__ __forceinline__ void wide_bulk(const uint8_t* q, uint64_t nbulk, uint
     wide_step<kSha, kCrc>(C, t, h, crc_raw, b + 2 < nbulk);
   }
 }
-#else
-// Three blocks in flight per lane (four 16-word buffers, loop unrolled by four): for distinct data
-// in HBM, where the lanes' scattered 64-B reads (each from its own DRAM row) take longer.
-template <bool kAligned16, bool kSha, bool kCrc>
-__device__ __forceinline__ void wide_bulk(const uint8_t* q, uint64_t nbulk, uint64_t nmin, uint64_t nmax,
-                                          const uint8_t* dummy, const uint32_t (&t)[8][256], uint32_t (&h)[5],
-                                          uint32_t& crc_raw) {
-  auto src = [&](uint64_t b) { return b < nbulk ? q + 64 * b : dummy; };
-  uint32_t A[16], B[16], C[16], D[16];
-  if (nmax == 0) return;
-  load_block_le<kAligned16>(src(0), A);
-  load_block_le<kAligned16>(src(1), B);
-  load_block_le<kAligned16>(src(2), C);
-  uint64_t b = 0;
-  for (; b + 6 < nmin; b += 4) {  // uniform phase: blocks b..b+6 exist in every lane
-    const uint8_t* qb = q + 64 * b;
-    load_block_le<kAligned16>(qb + 192, D);
-    wide_step<kSha, kCrc>(A, t, h, crc_raw, true);
-    load_block_le<kAligned16>(qb + 256, A);
-    wide_step<kSha, kCrc>(B, t, h, crc_raw, true);
-    load_block_le<kAligned16>(qb + 320, B);
-    wide_step<kSha, kCrc>(C, t, h, crc_raw, true);
-    load_block_le<kAligned16>(qb + 384, C);
-    wide_step<kSha, kCrc>(D, t, h, crc_raw, true);
-  }
-  for (; b < nmax; b += 4) {  // ragged phase (A, B, C hold blocks b..b+2 or the dummy)
-    load_block_le<kAligned16>(src(b + 3), D);
-    wide_step<kSha, kCrc>(A, t, h, crc_raw, b < nbulk);
-    if (b + 1 >= nmax) break;
-    load_block_le<kAligned16>(src(b + 4), A);
-    wide_step<kSha, kCrc>(B, t, h, crc_raw, b + 1 < nbulk);
-    if (b + 2 >= nmax) break;
-    load_block_le<kAligned16>(src(b + 5), B);
-    wide_step<kSha, kCrc>(C, t, h, crc_raw, b + 2 < nbulk);
-    if (b + 3 >= nmax) break;
-    load_block_le<kAligned16>(src(b + 6), C);
-    wide_step<kSha, kCrc>(D, t, h, crc_raw, b + 3 < nbulk);
-  }
-}
-#endif
 template <bool kAligned16>
 __device__ __forceinline__ void wide_bulk_any(const uint8_t* q, uint64_t nbulk, uint64_t nmin, uint64_t nmax,
                                               const uint8_t* dummy, bool any_sha, bool any_crc,
-                                              const uint32_t (&t)[8][256], uint32_t (&h)[5], uint32_t& crc_raw) {
-  if (any_sha && any_crc) wide_bulk<kAligned16, true, true>(q, nbulk, nmin, nmax, dummy, t, h, crc_raw);
-  else if (any_sha) wide_bulk<kAligned16, true, false>(q, nbulk, nmin, nmax, dummy, t, h, crc_raw);
-  else if (any_crc) wide_bulk<kAligned16, false, true>(q, nbulk, nmin, nmax, dummy, t, h, crc_raw);
+                                              const uint32_t (&t)[8][256], uint32_t (&h)[5], uint32_t& crc_raw,
+                                              uint32_t* prog, uint32_t w, uint32_t nw) {
+  if (any_sha && any_crc) wide_bulk<kAligned16, true, true>(q, nbulk, nmin, nmax, dummy, t, h, crc_raw, prog, w, nw);
+  else if (any_sha) wide_bulk<kAligned16, true, false>(q, nbulk, nmin, nmax, dummy, t, h, crc_raw, prog, w, nw);
+  else if (any_crc) wide_bulk<kAligned16, false, true>(q, nbulk, nmin, nmax, dummy, t, h, crc_raw, prog, w, nw);
 }
 
 // Wave-wide minimum of a per-lane 64-bit value over the lanes where `use` holds (uniform
@@ -1384,19 +1374,23 @@ __device__ __forceinline__ uint64_t wave_max64(uint64_t v) {
 __device__ unsigned long long g_wide_stats[8192 * 6];
 #endif
 
-__global__ __launch_bounds__(64 * kWideWaves, EFES_WIDE_DEPTH == 3 ? 2 : 3) void wide_kernel(const efes_job* __restrict__ jobs, uint32_t njobs,
-                                                                  const Tables* __restrict__ tabs) {
+__global__ __launch_bounds__(64 * kWideWaves * kWideMaxWps, 1) void wide_kernel(const efes_job* __restrict__ jobs,
+                                                                                uint32_t njobs,
+                                                                                const Tables* __restrict__ tabs) {
 #ifdef EFES_WIDE_STATS
   const unsigned long long st_t0 = __builtin_amdgcn_s_memtime();
   const unsigned long long st_r0 = __builtin_amdgcn_s_memrealtime();
 #endif
   __shared__ __attribute__((aligned(16))) WideLDS L;
+  extern __shared__ __attribute__((aligned(16))) uint8_t wide_xs[];  // blockDim.x x kXStride (launch_wide)
   {
     const uint4* src = reinterpret_cast<const uint4*>(tabs->slice8);
     uint4* dst = reinterpret_cast<uint4*>(L.slice8);
     for (int i = threadIdx.x; i < (int)(sizeof(L.slice8) / 16); i += blockDim.x) dst[i] = src[i];
+    if (threadIdx.x < kWideWaves * kWideMaxWps) L.prog[threadIdx.x] = 0;
   }
   __syncthreads();
+  const uint32_t wv = threadIdx.x / 64, nwv = blockDim.x / 64;
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   const bool live = j < njobs;
   const efes_job jb = live ? jobs[j] : efes_job{};
@@ -1406,7 +1400,7 @@ __global__ __launch_bounds__(64 * kWideWaves, EFES_WIDE_DEPTH == 3 ? 2 : 3) void
   efes_crc32_state* cs = jb.crc32;
   const bool do_sha = live && st != nullptr, do_crc = live && cs != nullptr;
   const bool fin = live && (jb.flags & EFES_JOB_FINALIZE) != 0;
-  uint8_t* xl = L.xs[threadIdx.x];
+  uint8_t* xl = wide_xs + (size_t)threadIdx.x * kXStride;
   int32_t status = EFES_OK;
 
   uint32_t h[5] = {0, 0, 0, 0, 0};
@@ -1462,8 +1456,9 @@ __global__ __launch_bounds__(64 * kWideWaves, EFES_WIDE_DEPTH == 3 ? 2 : 3) void
   // the shortest message over ALL lanes (a lane without a job has nbulk 0: no uniform phase)
   const uint64_t nmin = wave_min64(nbulk, true);
   const uint8_t* dummy = reinterpret_cast<const uint8_t*>(tabs);  // 36 KiB of valid device memory
-  if (all16) wide_bulk_any<true>(q, nbulk, nmin, nmax, dummy, any_sha, any_crc, L.slice8, h, crc_raw);
-  else wide_bulk_any<false>(q, nbulk, nmin, nmax, dummy, any_sha, any_crc, L.slice8, h, crc_raw);
+  if (all16) wide_bulk_any<true>(q, nbulk, nmin, nmax, dummy, any_sha, any_crc, L.slice8, h, crc_raw, L.prog, wv, nwv);
+  else wide_bulk_any<false>(q, nbulk, nmin, nmax, dummy, any_sha, any_crc, L.slice8, h, crc_raw, L.prog, wv, nwv);
+  if ((threadIdx.x & 63) == 0) __atomic_store_n(&L.prog[wv], 0xffffffffu, __ATOMIC_RELAXED);  // done: never the slowest
 #ifdef EFES_WIDE_STATS
   const unsigned long long st_t1 = __builtin_amdgcn_s_memtime();
 #endif
@@ -1630,9 +1625,29 @@ hipError_t launch_fed(const efes_job* jobs, uint32_t njobs, const Tables* tabs, 
 hipError_t launch_wide(const efes_job* jobs, uint32_t njobs, const Tables* tabs, hipStream_t s, bool exclusive,
                        int cus) {
   if (njobs == 0) return hipSuccess;
-  const uint32_t per = 64 * kWideWaves;
-  (void)cus;
-  return launch_reserving(wide_kernel, dim3((njobs + per - 1) / per), dim3(per), exclusive, s, jobs, njobs, tabs);
+  // waves per SIMD of the launch: a workgroup per CU holds all of its SIMDs' waves (wide_pace);
+  // exclusive parts (one wave per SIMD on reserved CUs) and EFES_WIDE_PACE=0 use 4-wave groups.
+  const uint64_t waves = (njobs + 63) / 64, simds = 4ull * (uint64_t)(cus > 0 ? cus : 256);
+  static const bool pace_off = [] {
+    const char* e = getenv("EFES_WIDE_PACE");
+    return e && *e == '0';
+  }();
+  const uint32_t wps = exclusive || pace_off ? 1u : (uint32_t)std::min<uint64_t>(kWideMaxWps, (waves + simds - 1) / simds);
+  const uint32_t per = 64 * kWideWaves * wps;
+  const size_t xs = (size_t)per * kXStride;  // the lanes' tail buffers (dynamic LDS)
+  size_t dyn = xs;
+  if (exclusive) {
+    hipFuncAttributes fa{};
+    if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(wide_kernel)) == hipSuccess &&
+        fa.sharedSizeBytes + xs < kCuLds)
+      dyn = kCuLds - fa.sharedSizeBytes;  // reserve the CU's LDS: no other workgroup on its SIMDs
+  }
+  if (dyn > 48 * 1024 &&
+      hipFuncSetAttribute(reinterpret_cast<const void*>(wide_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)dyn) != hipSuccess)
+    dyn = xs;
+  hipLaunchKernelGGL(wide_kernel, dim3((njobs + per - 1) / per), dim3(per), dyn, s, jobs, njobs, tabs);
+  return hipGetLastError();
 }
 
 #ifdef EFES_FED_STATS

@@ -63,13 +63,15 @@ using efes::Digest;
 
 namespace {
 
-// Shared queue sizing: EFES_DIGEST_STAGING_MIB of pinned staging in 64 KiB chunks (default
-// 256 MiB = 4096 chunks, so up to 4095 digests hold an upload at once).
+// Shared queue sizing: EFES_DIGEST_STAGING_MIB of pinned staging (default 256 MiB) in chunks of
+// EFES_DIGEST_CHUNK_KIB (default 64 KiB: 4096 chunks, so up to 4095 digests hold an upload at once).
 efes_queue* create_digest_queue(efes_ctx* ctx, int* rc) {
-  uint64_t mib = 256;
+  uint64_t mib = 256, kib = 64;
   if (const char* e = getenv("EFES_DIGEST_STAGING_MIB")) mib = strtoull(e, nullptr, 10);
+  if (const char* e = getenv("EFES_DIGEST_CHUNK_KIB")) kib = strtoull(e, nullptr, 10);
   if (mib < 1) mib = 1;
-  const uint64_t chunk = 64 << 10;
+  if (kib < 4 || kib > 4096) kib = 64;
+  const uint64_t chunk = kib << 10;
   const uint32_t chunks = (uint32_t)((mib << 20) / chunk) < 16 ? 16u : (uint32_t)((mib << 20) / chunk);
   efes_queue* q = nullptr;
   *rc = efes_queue_create(ctx, chunk, chunks, chunks - 1, &q);

@@ -299,6 +299,19 @@ def receiver_leg():
         res["phases"] = {"value": ph["value"], "cpu_s_per_gib": ph.get("cpu_s_per_gib"),
                          "request_threads_cpu_s_per_gib": ph.get("request_threads_cpu_s_per_gib"),
                          "phase_cpu_s_per_gib": ph.get("phase_cpu_s_per_gib")}
+        # the reference's saveFile with its digests on the CPU port (oracle/receiver_cpu: the same
+        # file work, SHA-1 + CRC-32 in MultiWriter order on 16 threads = the box's host cores)
+        from oracle import oracle
+
+        oracle.build()
+        rc = subprocess.run([os.path.join(ROOT, "oracle", "receiver_cpu"), d, "16", "64", str(4 << 20)], check=True,
+                            capture_output=True, text=True, timeout=300)
+        cres = json.loads(rc.stdout.strip().splitlines()[-1])
+        res["cpu_port"] = {"value": cres["value"], "unit": "GiB/s", "cores": 16, "kind": "port",
+                           "digests_match": cres["sum_sha1_crc32"] == want and cres["all_sums_equal"],
+                           "sample": f"oracle/receiver_cpu: {cres['uploads']} one-PATCH uploads x 4 MiB, saveFile's file "
+                                     f"work + SHA-1/CRC-32 on the CPU port, 16 threads, {cres['seconds']} s"}
+        res["vs_cpu_port"] = round(res["value"] / cres["value"], 2)
         out["receiver"] = res
         r = run(["sha1file", d, "256", "4", str(4 << 20)])
         r["digests_match"] = r.pop("sum_sha1") == hashlib.sha1(src).hexdigest() and r.pop("all_sums_equal")

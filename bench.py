@@ -322,7 +322,7 @@ def receiver_leg():
     return out
 
 
-def drain_leg(workers=(1, 16, 64, 256, 512), file_bytes: int = 4 << 20, cpu_threads: int = 16):
+def drain_leg(workers=(1, 16, 64, 256, 384, 512), file_bytes: int = 4 << 20, cpu_threads: int = 16):
     """The drainer's read-back (drain.go:87-125 -> write.go:68-117 sendFile ->
     sha1file.go): files on tmpfs moved by K concurrent workers through the C++ sendFile/Sha1File
     mirror, every read hashed on the GPU (their streams batched by the digest queue), to a sink
@@ -613,8 +613,10 @@ def ingest_spot_check(data, batches, config) -> bool:
 def concurrency_leg(args, ctx, device: str, stream):
     """How the rate of 4 MiB chunks depends on how many are in flight: one AUTO
     launch per count (DEEP up to one chunk per SIMD, FED4 / FED4E up to 32 / 48 per CU, GROUP4,
-    then WIDE),
-    chunks aliasing a 64 GiB device pool; one warm-up and two timed launches per point."""
+    then WIDE) over distinct bytes: up to 16 384 chunks (64 GiB) whole, beyond that each chunk as
+    four 1 MiB segment Writes with the states resident (as the configs[4] leg), since 4 MiB x 65 536
+    does not fit in HBM -- aliased chunks would be served from the caches.  One warm-up and two
+    timed passes per point."""
     import numpy as np
     import torch
 
@@ -622,23 +624,29 @@ def concurrency_leg(args, ctx, device: str, stream):
     from efes_amd.batch import DeviceBatch
 
     names = kernel_names()
-    chunk, pool = 4 << 20, 64 << 30
+    chunk, seg = 4 << 20, 1 << 20
     points = []
     with torch.cuda.stream(stream):
-        data = torch.empty(pool, dtype=torch.uint8, device=device)
-        ctx.fill_synthetic(data.data_ptr(), pool, 0xC0C0, stream.cuda_stream)
-        slots = pool // chunk
         for n in (1024, 2048, 4096, 8192, 16384, 65536, 196608):
-            b = DeviceBatch(data.data_ptr(), (np.arange(n, dtype=np.uint64) % np.uint64(slots)) * np.uint64(chunk),
-                            np.full(n, chunk), fresh=True, ctx=ctx, device=device)
-            wall, kernel_ms = run_timed([b], 2, 1, MODE_AUTO, device, stream, None)
+            whole = n * chunk <= 64 << 30
+            piece = chunk if whole else seg
+            data = torch.empty(n * piece, dtype=torch.uint8, device=device)
+            ctx.fill_synthetic(data.data_ptr(), n * piece, 0xC0C0, stream.cuda_stream)
+            offs = np.arange(n, dtype=np.uint64) * np.uint64(piece)
+            if whole:
+                batches = [DeviceBatch(data.data_ptr(), offs, np.full(n, chunk), fresh=True, ctx=ctx, device=device)]
+            else:
+                base = DeviceBatch(data.data_ptr(), offs, np.full(n, seg), ctx=ctx, device=device)
+                batches = [base.variant(fresh=k == 0, finalize=k == 3) for k in range(4)]
+            wall, kernel_ms = run_timed(batches, 2 * len(batches), 1, MODE_AUTO, device, stream, None)
             points.append({"chunks": n, "kernel": names[lib().efes_auto_mode(ctx.handle, n)],
-                           "GiB/s": round(2 * n * chunk / wall / GiB, 1), "ms_per_launch": round(kernel_ms, 2)})
-            del b
-        del data
-        torch.cuda.empty_cache()
+                           "segments": len(batches), "GiB/s": round(2 * n * chunk / wall / GiB, 1),
+                           "ms_per_launch": round(kernel_ms, 2)})
+            del batches, data
+            torch.cuda.empty_cache()
     return {"unit": "GiB/s", "chunk_bytes": chunk, "points": points,
-            "note": "one launch of n fresh 4 MiB chunks (fused SHA-1+CRC32), AUTO shape; not `value`"}
+            "note": "n fresh 4 MiB chunks (fused SHA-1+CRC32), AUTO shape, distinct bytes (segments = 1 MiB Writes "
+                    "per chunk when n x 4 MiB exceeds 64 GiB); not `value`"}
 
 
 def mixed_leg(args, rank: int, world: int, ctx, device: str, stream):

@@ -1635,17 +1635,33 @@ hipError_t launch_wide(const efes_job* jobs, uint32_t njobs, const Tables* tabs,
   const uint32_t wps = exclusive || pace_off ? 1u : (uint32_t)std::min<uint64_t>(kWideMaxWps, (waves + simds - 1) / simds);
   const uint32_t per = 64 * kWideWaves * wps;
   const size_t xs = (size_t)per * kXStride;  // the lanes' tail buffers (dynamic LDS)
-  size_t dyn = xs;
-  if (exclusive) {
-    hipFuncAttributes fa{};
-    if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(wide_kernel)) == hipSuccess &&
-        fa.sharedSizeBytes + xs < kCuLds)
-      dyn = kCuLds - fa.sharedSizeBytes;  // reserve the CU's LDS: no other workgroup on its SIMDs
+  // The kernel's static LDS, and the dynamic-LDS limit raised once to the rest of the CU's LDS
+  // (per launch `dyn` decides what a workgroup takes).
+  // Per device (the attribute is set on the current one; the caller holds a DeviceGuard).
+  static std::mutex mu;
+  static int8_t ok_dev[64] = {};  // 0 = not tried, 1 = raised, -1 = failed
+  static size_t static_lds = 0;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  bool big_ok = false;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    int8_t& st = ok_dev[dev & 63];
+    if (st == 0) {
+      hipFuncAttributes fa{};
+      st = -1;
+      if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(wide_kernel)) == hipSuccess) {
+        static_lds = fa.sharedSizeBytes;
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(wide_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kCuLds - static_lds)) == hipSuccess)
+          st = 1;
+      }
+    }
+    big_ok = st == 1;
   }
-  if (dyn > 48 * 1024 &&
-      hipFuncSetAttribute(reinterpret_cast<const void*>(wide_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)dyn) != hipSuccess)
-    dyn = xs;
+  if (!big_ok && xs > 48 * 1024) return hipErrorInvalidConfiguration;
+  // exclusive: reserve the CU's whole LDS, so no other workgroup shares its SIMDs
+  const size_t dyn = exclusive && big_ok ? kCuLds - static_lds : xs;
   hipLaunchKernelGGL(wide_kernel, dim3((njobs + per - 1) / per), dim3(per), dyn, s, jobs, njobs, tabs);
   return hipGetLastError();
 }

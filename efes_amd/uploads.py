@@ -56,6 +56,14 @@ class Upload:
         cs = ctypes.byref(Crc32State(crc & 0xFFFFFFFF)) if crc is not None else None
         check(lib().efes_upload_open(queue.handle, hashes, st, cs, ctypes.byref(h)), "efes_upload_open")
         self._h = h
+        self._view = None  # the last reservation's view, released when the reservation ends
+
+    def _end_reservation(self) -> None:
+        """A reservation lasts until the next call on the upload: its staging chunk may be handed to
+        the dispatcher (and reused) after that, so the view is released and any later use raises."""
+        if self._view is not None:
+            self._view.release()
+            self._view = None
 
     def write(self, p) -> int:
         """Write(p) of filereceiver.go:209's MultiWriter: staged (copied) before returning."""
@@ -66,6 +74,7 @@ class Upload:
             ptr, n = a.ctypes.data, a.size
         if isinstance(ptr, bytearray):
             ptr = (ctypes.c_char * n).from_buffer(ptr)
+        self._end_reservation()
         check(lib().efes_upload_write(self._h, ptr, n), "Upload.write")
         return n
 
@@ -73,17 +82,22 @@ class Upload:
         """efes_upload_reserve: a writable view of >= min(min_bytes, chunk) bytes of the upload's
         pinned staging chunk (zero-copy: fill it, then commit(k))."""
         p, n = ctypes.c_void_p(), ctypes.c_size_t()
+        self._end_reservation()
         check(lib().efes_upload_reserve(self._h, min_bytes, ctypes.byref(p), ctypes.byref(n)), "Upload.reserve")
-        return memoryview((ctypes.c_uint8 * n.value).from_address(p.value)).cast("B")
+        self._view = memoryview((ctypes.c_uint8 * n.value).from_address(p.value)).cast("B")
+        return self._view
 
     def commit(self, k: int) -> None:
         """efes_upload_commit: the first k reserved bytes are one Write(p[:k]) (sha1.go:58-79)."""
+        self._end_reservation()
         check(lib().efes_upload_commit(self._h, k), "Upload.commit")
 
     def flush(self) -> None:
+        self._end_reservation()
         check(lib().efes_upload_flush(self._h), "Upload.flush")
 
     def state(self) -> tuple[Sha1State, int]:
+        self._end_reservation()
         st, cs = Sha1State(), Crc32State()
         check(lib().efes_upload_state(self._h, ctypes.byref(st), ctypes.byref(cs)), "Upload.state")
         return st, cs.crc
@@ -91,6 +105,7 @@ class Upload:
     def sums(self) -> tuple[bytes, int]:
         """(SHA-1 Sum, CRC-32 Sum32) of everything written so far; the state is unchanged."""
         out = (ctypes.c_uint8 * 24)()
+        self._end_reservation()
         check(lib().efes_upload_sum(self._h, out), "Upload.sums")
         b = bytes(out)
         return b[:20], int.from_bytes(b[20:], "big")
@@ -105,6 +120,8 @@ class Upload:
         return a.raw[:200], c.raw[:8]
 
     def close(self) -> None:
+        if getattr(self, "_view", None) is not None:
+            self._end_reservation()
         if getattr(self, "_h", None):
             lib().efes_upload_close(self._h)
             self._h = None

@@ -667,11 +667,13 @@ def test_upload_reserve_commit_equals_write(env, oracle):
         with pytest.raises(efes.EfesError) as e:
             up.commit(8)
         assert e.value.code == efes.EFES_ERR_ARG
-        up.reserve(64)
+        stale = up.reserve(64)
         up.write(b"x")
         with pytest.raises(efes.EfesError) as e:
             up.commit(1)
         assert e.value.code == efes.EFES_ERR_ARG
+        with pytest.raises(ValueError):  # the Python view of an ended reservation is released
+            stale[0] = 1
         up.close()
 
 

@@ -1119,6 +1119,31 @@ def test_full_size_mixed_config_plan_equals_wide(env):
     torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("m", [100_000, 196_608])
+def test_wide_paced_ragged_launch_every_job(env, m):
+    """WIDE with 2 and 3 waves per SIMD (the paced shape launch_wide picks above 65 536 jobs,
+    efes_kernels.hip wide_pace) over RAGGED lengths 0..3000 at unaligned offsets: the ragged
+    loop, the tail buffer in dynamic LDS and the per-lane finalisation of every job against
+    hashlib/zlib (filereceiver.go:208-209 on each chunk)."""
+    torch = env["torch"]
+    pool = 64 << 20
+    buf = torch.empty(pool, dtype=torch.uint8, device="cuda:0")
+    env["ctx"].fill_synthetic(buf.data_ptr(), pool, 0x5EED + m, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    rng = np.random.default_rng(m)
+    lengths = rng.integers(0, 3001, m).astype(np.uint64)
+    lengths[:7] = [0, 1, 55, 56, 63, 64, 3000]
+    offs = rng.integers(0, pool - 3001, m).astype(np.uint64)
+    b = env["DeviceBatch"](buf.data_ptr(), offs, lengths, fresh=True, ctx=env["ctx"])
+    b.run(env["efes"].MODE_WIDE)
+    assert (b.status_host() == 0).all()
+    shas, crcs = b.sha1_hex(), b.crc_sum()
+    host = buf.cpu().numpy()
+    for i in range(m):
+        d = host[int(offs[i]):int(offs[i]) + int(lengths[i])].tobytes()
+        assert shas[i] == hashlib.sha1(d).hexdigest() and crcs[i] == zlib.crc32(d), (i, len(d))
+
+
 def test_full_size_ingest_launch_wide_equals_group4(env):
     """One BASELINE configs[4] launch at full size (196 608 x 4 MiB, chunks aliasing pool slots as
     bench.py's ingest leg does): WIDE (the shape AUTO picks) and GROUP4 agree on every digest,

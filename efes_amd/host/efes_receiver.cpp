@@ -667,6 +667,7 @@ struct FdGuard {
 
 namespace {
 std::atomic<bool> g_phases_on{false};
+std::atomic<clockid_t> g_phase_clock{CLOCK_THREAD_CPUTIME_ID};
 std::atomic<uint64_t> g_phase_ns[kPhases];
 const char* const kPhaseNames[kPhases] = {"create", "open", "reserve", "read", "write", "commit", "sync", "sum",
                                           "info"};
@@ -674,17 +675,19 @@ const char* const kPhaseNames[kPhases] = {"create", "open", "reserve", "read", "
 // Charges the calling thread's CPU time (user + system) since the last mark to a phase (when
 // enabled): with hundreds of request threads on 16 cores, wall time per phase would mostly be
 // run-queue waits.
-uint64_t thread_cpu_ns() {
+// EFES_RECEIVER_PHASE_CLOCK=wall charges wall time instead (where a request WAITS: run queue,
+// locks, pacing, its GPU chain).
+uint64_t phase_ns() {
   struct timespec ts;
-  clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
+  clock_gettime(g_phase_clock.load(std::memory_order_relaxed), &ts);
   return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
 }
 struct PhaseClock {
   bool on = g_phases_on.load(std::memory_order_relaxed);
-  uint64_t t = on ? thread_cpu_ns() : 0;
+  uint64_t t = on ? phase_ns() : 0;
   void mark(SavePhase p) {
     if (!on) return;
-    const uint64_t now = thread_cpu_ns();
+    const uint64_t now = phase_ns();
     g_phase_ns[p].fetch_add(now - t, std::memory_order_relaxed);
     t = now;
   }
@@ -692,6 +695,8 @@ struct PhaseClock {
 }  // namespace
 
 void EnableSavePhases(bool on) {
+  const char* c = getenv("EFES_RECEIVER_PHASE_CLOCK");
+  g_phase_clock.store(c && !strcmp(c, "wall") ? CLOCK_MONOTONIC : CLOCK_THREAD_CPUTIME_ID, std::memory_order_relaxed);
   for (auto& v : g_phase_ns) v.store(0, std::memory_order_relaxed);
   g_phases_on.store(on, std::memory_order_relaxed);
 }

@@ -249,7 +249,20 @@ int main(int argc, char** argv) {
       snprintf(b, sizeof b, "}, \"request_threads_cpu_s_per_gib\": %.4f, \"unlink_cpu_s_per_gib\": %.4f",
                req_cpu_ns.load() * 1e-9 / gib, unlink_cpu_ns.load() * 1e-9 / gib);
       phase_json += b;
+      const char* pc = getenv("EFES_RECEIVER_PHASE_CLOCK");
+      snprintf(b, sizeof b, ", \"phase_clock\": \"%s\"", pc && !strcmp(pc, "wall") ? "wall" : "thread_cpu");
+      phase_json += b;
       EnableSavePhases(false);
+    }
+    {  // launches of the batching queue(s): jobs per launch = uploads hashed side by side
+      efes_queue_stats qs{};
+      uint64_t launches = 0, jobs = 0;
+      for (size_t g = 0; g < ctxs.size(); ++g)
+        if (efes_queue_get_stats(h->queue(g), &qs) == EFES_OK) launches += qs.launches, jobs += qs.jobs;
+      char b[128];
+      snprintf(b, sizeof b, ", \"queue_launches\": %llu, \"jobs_per_launch\": %.1f", (unsigned long long)launches,
+               launches ? (double)jobs / launches : 0.0);
+      phase_json += b;
     }
     delete h;
     for (size_t g = 1; g < ctxs.size(); ++g) efes_ctx_destroy(ctxs[g]);

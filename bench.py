@@ -322,12 +322,16 @@ def receiver_leg():
     return out
 
 
-def drain_leg(workers=(1, 16, 64, 256, 384, 512), file_bytes: int = 4 << 20, cpu_threads: int = 16):
+def drain_leg(workers=(1, 16, 64, 128, 192, 256, 512), file_bytes: int = 4 << 20, cpu_threads: int = 16,
+              files_per_worker: int = 16):
     """The drainer's read-back (drain.go:87-125 -> write.go:68-117 sendFile ->
     sha1file.go): files on tmpfs moved by K concurrent workers through the C++ sendFile/Sha1File
     mirror, every read hashed on the GPU (their streams batched by the digest queue), to a sink
     server; against the CPU port -- the oracle's sha1digest over the same files in 32 KiB reads on
-    `cpu_threads` host threads.  Reports the K at which the GPU path overtakes the CPU."""
+    `cpu_threads` host threads.  Reports the K at which the GPU path overtakes the CPU.  Each worker
+    moves `files_per_worker` files one after the other (16: the steady state; with 4 the workers'
+    start and the last files' chains -- 46 ms each -- were a third of the run,
+    profiles/r03_drain/drain_stats.log)."""
     import hashlib
     import subprocess
     import tempfile
@@ -345,11 +349,12 @@ def drain_leg(workers=(1, 16, 64, 256, 384, 512), file_bytes: int = 4 << 20, cpu
             with open(os.path.join(d, f"{i}.fid"), "wb") as f:
                 f.write(src)
         for k in workers:
-            fids = max(8, 4 * k)
+            fids = max(8, files_per_worker * k)
             r = subprocess.run([exe, "drain", d, str(k), str(fids), str(file_bytes), str(nfiles)], check=True,
                                capture_output=True, text=True, timeout=300)
             res = json.loads(r.stdout.strip().splitlines()[-1])
             points.append({"workers": k, "fids": fids, "GiB/s": res["value"],
+                           "cpu_s_per_gib": res.get("cpu_s_per_gib"), "jobs_per_launch": res.get("jobs_per_launch"),
                            "digests_match": res["sum_sha1"] == want and res["all_sums_equal"] and not res["errors"]})
 
         # the CPU port: oracle/drain_cpu (sha1digest's generic block restated in C, 32 KiB reads through

@@ -445,6 +445,11 @@ int main(int argc, char** argv) {
     ClientConfig cfg;
     cfg.Drainer = true;  // efes-drain: true (write.go:163-165)
     std::atomic<long> next{0};
+    efes_pool* stats_pool = nullptr;  // only to read the digest queue's launch counters
+    efes_queue_stats q0{}, q1{};
+    if (efes_pool_create(&ctx, 1, &stats_pool) == EFES_OK) (void)efes_pool_stats(stats_pool, 0, &q0);
+    double s0 = 0, s1 = 0;
+    const double c0 = cpu_seconds(&s0);
     auto t0 = std::chrono::steady_clock::now();
     std::vector<std::thread> th;
     for (int t = 0; t < T; ++t)
@@ -468,11 +473,17 @@ int main(int argc, char** argv) {
       });
     for (auto& x : th) x.join();
     secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    const double cpu_s = cpu_seconds(&s1) - c0, gib = (double)F * S / (1u << 30);
+    if (stats_pool) (void)efes_pool_stats(stats_pool, 0, &q1);
+    efes_pool_destroy(stats_pool);
+    const uint64_t nl = q1.launches - q0.launches;
     printf("{\"workload\": \"drain\", \"pinned_cpus\": %d, \"workers\": %d, \"files\": %ld, \"file_bytes\": %zu, "
            "\"read_bytes\": 32768, \"dir_fs\": \"%s\", \"seconds\": %.4f, \"value\": %.3f, \"unit\": \"GiB/s\", "
-           "\"sum_sha1\": \"%s\", \"all_sums_equal\": %s, \"errors\": %d}\n",
-           pinned_cpus, T, F, S, fs_name(dir), secs, (double)F * S / secs / (1u << 30), first.c_str(),
-           bad ? "false" : "true", errs.load());
+           "\"sum_sha1\": \"%s\", \"all_sums_equal\": %s, \"errors\": %d, \"cpu_s_per_gib\": %.4f, \"sys_share\": %.3f, "
+           "\"queue_launches\": %llu, \"jobs_per_launch\": %.1f}\n",
+           pinned_cpus, T, F, S, fs_name(dir), secs, gib / secs, first.c_str(), bad ? "false" : "true", errs.load(),
+           cpu_s / gib, cpu_s > 0 ? (s1 - s0) / cpu_s : 0.0, (unsigned long long)nl,
+           nl ? (double)(q1.jobs - q0.jobs) / nl : 0.0);
   } else {
     fprintf(stderr, "unknown mode %s\n", mode.c_str());
     return 2;

@@ -243,11 +243,16 @@ int take_chunk(efes_upload* u, std::unique_lock<std::mutex>& lk) {
 // gains nothing from more (its chain takes one chunk per launch: one in the running launch, one
 // in the launch queued behind it, one pending for the launch after), while a fast writer that
 // grabs every free chunk leaves the other uploads nothing to put in the next launches.
-// EFES_QUEUE_AHEAD overrides kAhead (0: no per-upload cap).
+// EFES_QUEUE_AHEAD overrides kAhead (0: no per-upload cap).  "Scarce" = no more free chunks than
+// uploads OPEN now (each may need one to go on), not than the queue's capacity: the shared digest
+// queue has max_uploads = chunks - 1, so a capacity test paced every digest always -- and its
+// writers then slept and woke once per 64 KiB chunk (drainer at 512 files: 17-19 GiB/s paced from
+// the first chunk, 24-26 with room to run ahead; profiles/r03_drain/drain_pace.log).
 constexpr uint64_t kAhead = 3;
 void pace(efes_upload* u, std::unique_lock<std::mutex>& lk) {
   efes_queue* q = u->q;
-  if (q->ahead && q->free_chunks.size() <= (size_t)q->max_uploads)
+  const size_t open = (size_t)q->max_uploads - q->free_states.size();
+  if (q->ahead && q->free_chunks.size() <= open)
     u->done.wait(lk, [&] { return q->fault || u->inflight < q->ahead; });
 }
 

@@ -468,9 +468,10 @@ def make_workload(args, rank: int, world: int, ctx, device: str, stream):
 # Instruction-issue ceilings: a wave64 integer VALU instruction holds its SIMD
 # for 4 cycles (SQ_INSTS_VALU == SQ_ACTIVE_INST_VALU quad-cycles in profiles/r01_pmc), and
 #   DEEP: one message per wave; its SHA-1 chain is 405 VALU per 64-B block (80 rounds x 5 + 5);
-#   WIDE: one message per lane; 725 VALU per 64-B block per wave (SQ_INSTS_VALU of a configs[4]
-#         launch: 592 SHA-1 rounds+schedule, 16 byte swaps, ~100 CRC-32 slicing-by-8 ops, loop;
-#         ~630 with SHA-1 only, from the ISA).
+#   WIDE: one message per lane; 717 VALU per 64-B block per wave (SQ_INSTS_VALU of a configs[4]
+#         launch, profiles/r03_wide_crc_pmc: 592 SHA-1 rounds+schedule, 16 byte swaps, 97 CRC-32 ops
+#         from the position tables, loop; 725 with round 3's slicing-by-8; ~630 with SHA-1 only,
+#         from the ISA).
 CLOCK_HZ = 2.4e9
 N_SIMD = 1024
 VALU_CYC = 4
@@ -482,7 +483,7 @@ def binding_roofline(kernel: str, achieved_gbs: float, concurrent_msgs: int, sha
         model = ("serial SHA-1 chain: each of min(messages, 1024 SIMDs) messages advances one 64-B block per "
                  "405 VALU x 4 cycles at 2.4 GHz (one wave per message)")
     else:
-        per_block = 630 if sha1_only else 725
+        per_block = 630 if sha1_only else 717
         lanes = min(concurrent_msgs, N_SIMD * 64 * 8)
         ceiling = min(lanes / 64, N_SIMD) * 64 * 64 * CLOCK_HZ / (per_block * VALU_CYC) / 1e9
         model = (f"VALU issue: {per_block} VALU per 64-B block per wave of 64 messages, 4 cycles each, "

@@ -1193,10 +1193,29 @@ constexpr int kWideWaves = 4;    // waves per workgroup per SIMD-wave (one per S
 constexpr int kWideMaxWps = 3;   // waves per SIMD that fit (132 VGPRs)
 constexpr int kXStride = 68;
 
+// WIDE's CRC tables in LDS: the position tables (crc_issue below), or slicing-by-8's.
+#ifndef EFES_WIDE_SLICE8
+using WideCrcTab = uint32_t[64][256];
+#else
+using WideCrcTab = uint32_t[8][256];
+#endif
+
 struct WideLDS {
-  uint32_t slice8[8][256];
+  WideCrcTab crc;  // PosTables (64 KiB), or slice8 (8 KiB) with -DEFES_WIDE_SLICE8
   uint32_t prog[kWideWaves * kWideMaxWps];  // blocks done by each wave of the workgroup
 };
+#ifndef EFES_WIDE_SLICE8
+// The byte-wise head/tail: pos[63][b] (byte b, no byte after it) is IEEETable[b] (crc32.go:125).
+__device__ __forceinline__ const uint32_t* wide_t0(const WideLDS& L) { return L.crc[63]; }
+__device__ __forceinline__ const uint4* wide_tab_src(const Tables* tabs) {
+  return reinterpret_cast<const uint4*>(tabs + 1);  // PosTables follow Tables (efes_ctx_create)
+}
+#else
+__device__ __forceinline__ const uint32_t* wide_t0(const WideLDS& L) { return L.crc[0]; }
+__device__ __forceinline__ const uint4* wide_tab_src(const Tables* tabs) {
+  return reinterpret_cast<const uint4*>(tabs->slice8);
+}
+#endif
 
 // The priority of wave w from its SIMD siblings' progress (w % 4, w % 4 + 4, ...): the furthest
 // behind gets 3, the furthest ahead 0, the rest 1.  Wave-uniform; `b` = blocks this wave has done.
@@ -1234,50 +1253,84 @@ __device__ __forceinline__ uint32_t fin_byte(const uint8_t* xl, uint32_t i, uint
 // computes both and never stores the other.  Lanes run their own trip counts; with jobs
 // sorted by length the lanes of a wave finish together.
 
-// One slicing-by-8 step (8 bytes = LE words 2S, 2S+1) of crc_words_raw, split in two: the eight
-// table lookups are issued first, the XORs that consume them come five SHA-1 rounds later.
+// The block's raw CRC from the position tables (pos[o][b]: the register after a 64-byte block
+// whose only nonzero byte is b at offset o; efes_internal.hpp): crc32.go:153-169's slicing over
+// the whole block at once.  The register is linear, so the new register is the XOR of 64
+// lookups, and only the first four (bytes 0..3 XOR the old register, crc32.go:157) depend on the
+// previous block.  Split in eight groups of eight bytes (LE words 2S, 2S+1): a group's lookups are
+// issued first, the XORs that fold them into the running value come five SHA-1 rounds later.
+// 97 VALU per block (64 lookup addresses, 1 + 32 XORs) against 112 for slicing-by-8's eight
+// dependent steps (`-DEFES_WIDE_SLICE8`, kept for A/B).
 struct CrcPending {
   uint32_t v[8];
 };
+#ifndef EFES_WIDE_SLICE8
 template <int S>
-__device__ __forceinline__ void crc_issue(const uint32_t (&t)[8][256], uint32_t crc, const uint32_t (&le)[16],
-                                          CrcPending& p) {
+__device__ __forceinline__ void crc_issue(const WideCrcTab& t, uint32_t crc, const uint32_t (&le)[16], CrcPending& p) {
+  const uint32_t lo = S == 0 ? crc ^ le[0] : le[2 * S];
+  const uint32_t hi = le[2 * S + 1];
+  constexpr int o = 8 * S;
+  p.v[0] = t[o + 0][lo & 0xffu]; p.v[1] = t[o + 1][(lo >> 8) & 0xffu]; p.v[2] = t[o + 2][(lo >> 16) & 0xffu];
+  p.v[3] = t[o + 3][lo >> 24]; p.v[4] = t[o + 4][hi & 0xffu]; p.v[5] = t[o + 5][(hi >> 8) & 0xffu];
+  p.v[6] = t[o + 6][(hi >> 16) & 0xffu]; p.v[7] = t[o + 7][hi >> 24];
+}
+// Group S's eight values folded into the running value `acc` (group 0 starts it).
+template <int S>
+__device__ __forceinline__ uint32_t crc_combine(const CrcPending& p, uint32_t acc) {
+  const uint32_t a = __builtin_amdgcn_bitop3_b32(p.v[0], p.v[1], p.v[2], 0x96);
+  const uint32_t b = __builtin_amdgcn_bitop3_b32(p.v[3], p.v[4], p.v[5], 0x96);
+  if constexpr (S == 0) return __builtin_amdgcn_bitop3_b32(a, b, p.v[6] ^ p.v[7], 0x96);
+  const uint32_t c = __builtin_amdgcn_bitop3_b32(acc, a, b, 0x96);
+  return __builtin_amdgcn_bitop3_b32(c, p.v[6], p.v[7], 0x96);
+}
+#else
+// One slicing-by-8 step (8 bytes = LE words 2S, 2S+1) of crc_words_raw.
+template <int S>
+__device__ __forceinline__ void crc_issue(const WideCrcTab& t, uint32_t crc, const uint32_t (&le)[16], CrcPending& p) {
   const uint32_t hi = le[2 * S + 1];
   const uint32_t c = crc ^ le[2 * S];
   p.v[0] = t[0][hi >> 24]; p.v[1] = t[1][(hi >> 16) & 0xffu]; p.v[2] = t[2][(hi >> 8) & 0xffu];
   p.v[3] = t[3][hi & 0xffu]; p.v[4] = t[4][c >> 24]; p.v[5] = t[5][(c >> 16) & 0xffu];
   p.v[6] = t[6][(c >> 8) & 0xffu]; p.v[7] = t[7][c & 0xffu];
 }
-__device__ __forceinline__ uint32_t crc_combine(const CrcPending& p) {
+template <int S>
+__device__ __forceinline__ uint32_t crc_combine(const CrcPending& p, uint32_t) {
   const uint32_t a = __builtin_amdgcn_bitop3_b32(p.v[0], p.v[1], p.v[2], 0x96);
   const uint32_t b = __builtin_amdgcn_bitop3_b32(p.v[3], p.v[4], p.v[5], 0x96);
   return __builtin_amdgcn_bitop3_b32(a, b, p.v[6] ^ p.v[7], 0x96);
 }
+#endif
 
-// 80 inline SHA-1 rounds with the 8 CRC steps of the same block woven in: step k's lookups are
-// issued after round 10k+4 and combined after round 10k+9, so the LDS latency of the CRC's
-// dependent lookups is covered by SHA-1 rounds.  Scheduling barriers every five rounds keep
-// the compiler from regrouping the CRC steps into back-to-back lookup/wait clusters.
+// 80 inline SHA-1 rounds with the 8 CRC groups of the same block woven in: group k's lookups are
+// issued after round 10k+4 and combined after round 10k+9, so the LDS latency of the lookups is
+// covered by SHA-1 rounds.  Scheduling barriers every five rounds keep the compiler from
+// regrouping the CRC groups into back-to-back lookup/wait clusters.  `crc` is the register
+// before the block until group 0 is issued, the running value after.
 template <int R, bool kSha, bool kCrc>
 struct WideRounds {
-  __device__ __forceinline__ static void run(uint32_t (&s)[5], uint32_t (&w)[16], const uint32_t (&t)[8][256],
-                                             uint32_t& crc, const uint32_t (&le)[16], CrcPending& p) {
+  __device__ __forceinline__ static void run(uint32_t (&s)[5], uint32_t (&w)[16], const WideCrcTab& t, uint32_t& crc,
+                                             const uint32_t (&le)[16], CrcPending& p) {
     if constexpr (kSha) round_inline<R>(s, w);
     if constexpr (kCrc && R % 10 == 4) crc_issue<R / 10>(t, crc, le, p);
-    if constexpr (kCrc && R % 10 == 9) crc = crc_combine(p);
+    if constexpr (kCrc && R % 10 == 9) {
+      crc = crc_combine<R / 10>(p, crc);
+      // Pins the fold here: the 64-term XOR is otherwise reassociated into one tree at the end of
+      // the block, with all 64 lookups live at once (168 VGPRs and spills).
+      asm volatile("" : "+v"(crc));
+    }
     if constexpr (kSha && kCrc && R % 5 == 4) __builtin_amdgcn_sched_barrier(0);
     WideRounds<R + 1, kSha, kCrc>::run(s, w, t, crc, le, p);
   }
 };
 template <bool kSha, bool kCrc>
 struct WideRounds<80, kSha, kCrc> {
-  __device__ __forceinline__ static void run(uint32_t (&)[5], uint32_t (&)[16], const uint32_t (&)[8][256], uint32_t&,
+  __device__ __forceinline__ static void run(uint32_t (&)[5], uint32_t (&)[16], const WideCrcTab&, uint32_t&,
                                              const uint32_t (&)[16], CrcPending&) {}
 };
 
 // One block of one lane's message; `live` lanes (b < their own block count) commit the result.
 template <bool kSha, bool kCrc>
-__device__ __forceinline__ void wide_step(const uint32_t (&le)[16], const uint32_t (&t)[8][256], uint32_t (&h)[5],
+__device__ __forceinline__ void wide_step(const uint32_t (&le)[16], const WideCrcTab& t, uint32_t (&h)[5],
                                           uint32_t& crc_raw, bool live) {
   uint32_t w[16];
 #pragma unroll
@@ -1306,7 +1359,7 @@ __device__ __forceinline__ void wide_step(const uint32_t (&le)[16], const uint32
 // both and never stores the other.  Jobs sorted by length keep the lanes of a wave equally long.
 template <bool kAligned16, bool kSha, bool kCrc>
 __device__ __forceinline__ void wide_bulk(const uint8_t* q, uint64_t nbulk, uint64_t nmin, uint64_t nmax,
-                                          const uint8_t* dummy, const uint32_t (&t)[8][256], uint32_t (&h)[5],
+                                          const uint8_t* dummy, const WideCrcTab& t, uint32_t (&h)[5],
                                           uint32_t& crc_raw, uint32_t* prog, uint32_t w, uint32_t nw) {
   auto src = [&](uint64_t b) { return b < nbulk ? q + 64 * b : dummy; };
   uint32_t A[16], B[16], C[16];
@@ -1339,7 +1392,7 @@ __device__ __forceinline__ void wide_bulk(const uint8_t* q, uint64_t nbulk, uint
 template <bool kAligned16>
 __device__ __forceinline__ void wide_bulk_any(const uint8_t* q, uint64_t nbulk, uint64_t nmin, uint64_t nmax,
                                               const uint8_t* dummy, bool any_sha, bool any_crc,
-                                              const uint32_t (&t)[8][256], uint32_t (&h)[5], uint32_t& crc_raw,
+                                              const WideCrcTab& t, uint32_t (&h)[5], uint32_t& crc_raw,
                                               uint32_t* prog, uint32_t w, uint32_t nw) {
   if (any_sha && any_crc) wide_bulk<kAligned16, true, true>(q, nbulk, nmin, nmax, dummy, t, h, crc_raw, prog, w, nw);
   else if (any_sha) wide_bulk<kAligned16, true, false>(q, nbulk, nmin, nmax, dummy, t, h, crc_raw, prog, w, nw);
@@ -1384,9 +1437,9 @@ __global__ __launch_bounds__(64 * kWideWaves * kWideMaxWps, 1) void wide_kernel(
   __shared__ __attribute__((aligned(16))) WideLDS L;
   extern __shared__ __attribute__((aligned(16))) uint8_t wide_xs[];  // blockDim.x x kXStride (launch_wide)
   {
-    const uint4* src = reinterpret_cast<const uint4*>(tabs->slice8);
-    uint4* dst = reinterpret_cast<uint4*>(L.slice8);
-    for (int i = threadIdx.x; i < (int)(sizeof(L.slice8) / 16); i += blockDim.x) dst[i] = src[i];
+    const uint4* src = wide_tab_src(tabs);
+    uint4* dst = reinterpret_cast<uint4*>(L.crc);
+    for (int i = threadIdx.x; i < (int)(sizeof(L.crc) / 16); i += blockDim.x) dst[i] = src[i];
     if (threadIdx.x < kWideWaves * kWideMaxWps) L.prog[threadIdx.x] = 0;
   }
   __syncthreads();
@@ -1445,7 +1498,7 @@ __global__ __launch_bounds__(64 * kWideWaves * kWideMaxWps, 1) void wide_kernel(
     pos = nh;
   }
   if (go && do_crc)
-    for (uint64_t i = 0; i < pos; ++i) crc_raw = crc_byte(L.slice8[0], crc_raw, ldg_u8(p + i));
+    for (uint64_t i = 0; i < pos; ++i) crc_raw = crc_byte(wide_t0(L), crc_raw, ldg_u8(p + i));
 
   // ---- bulk: lanes iterate their own block counts (masked when done)
   const uint8_t* q = p + pos;
@@ -1456,8 +1509,8 @@ __global__ __launch_bounds__(64 * kWideWaves * kWideMaxWps, 1) void wide_kernel(
   // the shortest message over ALL lanes (a lane without a job has nbulk 0: no uniform phase)
   const uint64_t nmin = wave_min64(nbulk, true);
   const uint8_t* dummy = reinterpret_cast<const uint8_t*>(tabs);  // 36 KiB of valid device memory
-  if (all16) wide_bulk_any<true>(q, nbulk, nmin, nmax, dummy, any_sha, any_crc, L.slice8, h, crc_raw, L.prog, wv, nwv);
-  else wide_bulk_any<false>(q, nbulk, nmin, nmax, dummy, any_sha, any_crc, L.slice8, h, crc_raw, L.prog, wv, nwv);
+  if (all16) wide_bulk_any<true>(q, nbulk, nmin, nmax, dummy, any_sha, any_crc, L.crc, h, crc_raw, L.prog, wv, nwv);
+  else wide_bulk_any<false>(q, nbulk, nmin, nmax, dummy, any_sha, any_crc, L.crc, h, crc_raw, L.prog, wv, nwv);
   if ((threadIdx.x & 63) == 0) __atomic_store_n(&L.prog[wv], 0xffffffffu, __ATOMIC_RELAXED);  // done: never the slowest
 #ifdef EFES_WIDE_STATS
   const unsigned long long st_t1 = __builtin_amdgcn_s_memtime();
@@ -1467,7 +1520,7 @@ __global__ __launch_bounds__(64 * kWideWaves * kWideMaxWps, 1) void wide_kernel(
   const uint64_t tpos = pos + (nbulk << 6);
   const uint32_t r = go ? (uint32_t)(plen - tpos) : 0u;
   if (do_crc)
-    for (uint32_t i = 0; i < r; ++i) crc_raw = crc_byte(L.slice8[0], crc_raw, ldg_u8(p + tpos + i));
+    for (uint32_t i = 0; i < r; ++i) crc_raw = crc_byte(wide_t0(L), crc_raw, ldg_u8(p + tpos + i));
   if (do_sha && r > 0) {
     for (uint32_t i = 0; i < r; ++i) xl[i] = ldg_u8(p + tpos + i);
     nx_new = r;

@@ -314,14 +314,16 @@ int efes_crc32_span(efes_ctx* ctx, const void* data, uint64_t length, efes_crc32
 }
 
 int efes_crc32_tables(uint32_t* out, size_t nwords) {
-  const size_t need = sizeof(Tables) / 4;
+  const size_t need = sizeof(Tables) / 4, with_pos = need + sizeof(efes::PosTables) / 4;
   if (!out || nwords < need) return EFES_ERR_ARG;
-  Tables* t = static_cast<Tables*>(malloc(sizeof(Tables)));
+  Tables* t = static_cast<Tables*>(malloc(sizeof(Tables) + sizeof(efes::PosTables)));
   if (!t) return EFES_ERR_NOMEM;
   efes::build_tables(t);
-  memcpy(out, t, sizeof(Tables));
+  const bool pos = nwords >= with_pos;  // room for the position tables too (WIDE / grouped kernels)
+  if (pos) efes::build_pos_tables(t, reinterpret_cast<efes::PosTables*>(t + 1));
+  memcpy(out, t, pos ? sizeof(Tables) + sizeof(efes::PosTables) : sizeof(Tables));
   free(t);
-  return (int)need;
+  return (int)(pos ? with_pos : need);
 }
 
 uint32_t efes_crc32_combine(uint32_t crc1, uint32_t crc2, uint64_t len2) {

@@ -320,7 +320,10 @@ int efes_crc32_unmarshal_text(efes_crc32* d, const char* text, size_t n);/* crc3
 
 /* Host-side diagnostics (no device work): copies the CRC-32 tables the kernels use,
  * slice8[8][256] (crc32.go:138-149) then shift[7][4][256] (advance of the raw register
- * over 64<<k zero bytes, byte-sliced); returns the word count written or EFES_ERR_ARG. */
+ * over 64<<k zero bytes, byte-sliced), then -- when nwords leaves room for them (9216 + 16384
+ * words) -- the position tables pos[64][256] (the raw register after a 64-byte block whose only
+ * nonzero byte is b at offset o, from register 0: the WIDE and grouped kernels' block CRC);
+ * returns the word count written or EFES_ERR_ARG. */
 int efes_crc32_tables(uint32_t* out, size_t nwords);
 
 /* CRC-32 of A||B from crc(A), crc(B) and |B| (crc32.go is GF(2)-linear: the zlib

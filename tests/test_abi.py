@@ -3,6 +3,7 @@ import ctypes
 import os
 import re
 import subprocess
+import zlib
 
 import numpy as np
 import pytest
@@ -108,6 +109,36 @@ def test_crc_tables(efes_lib, oracle):
                 got ^= int(shift[k, b, (v >> (8 * b)) & 0xFF])
             assert got == _advance_raw(t0, v, 64 << k), (k, hex(v))
     assert efes_lib.lib().efes_crc32_tables(buf.ctypes.data, n - 1) == efes_lib.EFES_ERR_ARG
+
+
+def test_position_table_block_update(efes_lib):
+    """The WIDE / grouped kernels' block CRC (efes_kernels.hip crc_issue / crc_block_pos): the raw
+    register after a 64-byte block is the XOR of pos[o][byte_o] over its 64 bytes, with bytes 0..3
+    XOR-ed with the old register first -- equal to crc32.go's byte-wise update (:125) and to zlib."""
+    n = 8 * 256 + 7 * 4 * 256
+    buf = np.zeros(n + 64 * 256, dtype=np.uint32)
+    assert efes_lib.lib().efes_crc32_tables(buf.ctypes.data, buf.size) == buf.size
+    t0, pos = buf[:256], buf[n:].reshape(64, 256)
+    assert (pos[63] == t0).all()  # a byte with nothing after it: IEEETable
+    rng = np.random.default_rng(5)
+    crc = 0  # Go's crc of "" (crc32.go:68); raw register = ~crc
+    data = b""
+    for _ in range(24):
+        block = rng.integers(0, 256, 64, dtype=np.uint8).tobytes()
+        reg = (~crc) & 0xFFFFFFFF
+        got = 0
+        for o, b in enumerate(block):
+            got ^= int(pos[o][b ^ ((reg >> (8 * o)) & 0xFF if o < 4 else 0)])
+        assert got == _advance_raw_bytes(t0, reg, block)
+        crc = (~got) & 0xFFFFFFFF
+        data += block
+        assert crc == zlib.crc32(data)
+
+
+def _advance_raw_bytes(t0, s, data):
+    for b in data:
+        s = int(t0[(s ^ b) & 0xFF]) ^ (s >> 8)
+    return s
 
 
 def test_no_gpu_is_an_error_not_a_fallback(efes_lib):

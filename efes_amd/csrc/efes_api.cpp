@@ -137,6 +137,21 @@ void efes::build_pos_tables(const Tables* t, PosTables* out) {
     }
 }
 
+// A stream on a hardware queue of its own (efes_internal.hpp).
+hipError_t efes::own_queue_stream(const efes_ctx* ctx, hipStream_t* out) {
+  static const bool plain = [] {
+    const char* e = getenv("EFES_PART_STREAMS");
+    return e && !strcmp(e, "plain");
+  }();
+  if (plain) return hipStreamCreateWithFlags(out, hipStreamNonBlocking);
+  uint32_t all_cus[8];
+  for (int w = 0; w < 8; ++w) {
+    const int left = ctx->cus - 32 * w;
+    all_cus[w] = left >= 32 ? 0xffffffffu : left > 0 ? (1u << left) - 1u : 0u;
+  }
+  return hipExtStreamCreateWithCUMask(out, (uint32_t)std::min(8, (ctx->cus + 31) / 32), all_cus);
+}
+
 // ======================================================================= C ABI
 extern "C" {
 
@@ -185,21 +200,9 @@ int efes_ctx_create(int device, efes_ctx** out) {
   hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming);
   // The part streams of a planned batch must land on distinct hardware queues, or parts meant to
-  // run side by side serialize (GPU_MAX_HW_QUEUES is 4 by default and HIP shares the queues among
-  // ALL the process's streams: configs[3] in a fresh process measured 1.03-1.09 s per step
-  // against 0.885 s with 8 queues).  A stream created with a CU mask gets a hardware queue of its
-  // own (the mask is a queue property); the mask here is every CU, so placement is unchanged.
-  // EFES_PART_STREAMS=plain restores ordinary streams (A/B).
-  const char* ps_env = getenv("EFES_PART_STREAMS");
-  const bool masked = !(ps_env && !strcmp(ps_env, "plain"));
-  uint32_t all_cus[8];
-  for (int w = 0; w < 8; ++w) {
-    const int lo = 32 * w, left = ctx->cus - lo;
-    all_cus[w] = left >= 32 ? 0xffffffffu : left > 0 ? (1u << left) - 1u : 0u;
-  }
-  for (int i = 0; i < EFES_PLAN_MAX_PARTS && e == hipSuccess; ++i)
-    e = masked ? hipExtStreamCreateWithCUMask(&ctx->side[i], (uint32_t)std::min(8, (ctx->cus + 31) / 32), all_cus)
-               : hipStreamCreateWithFlags(&ctx->side[i], hipStreamNonBlocking);
+  // run side by side serialize (configs[3] in a fresh process: 1.03-1.09 s per step on ordinary
+  // streams, 0.885 s with 8 queues or CU-masked streams).
+  for (int i = 0; i < EFES_PLAN_MAX_PARTS && e == hipSuccess; ++i) e = efes::own_queue_stream(ctx, &ctx->side[i]);
   for (int i = 0; i < EFES_PLAN_MAX_PARTS && e == hipSuccess; ++i)
     e = hipEventCreateWithFlags(&ctx->ev_join[i], hipEventDisableTiming);
   if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&ctx->d_tabs), tab_bytes);

@@ -202,7 +202,7 @@ int efes_hash_host(efes_ctx* ctx, const efes_job* jobs, uint32_t n, uint64_t seg
 
   Stream copy;
   Event copied[2], hashed[2];
-  e = hipStreamCreateWithFlags(&copy.s, hipStreamNonBlocking);
+  e = efes::own_queue_stream(ctx, &copy.s);  // never behind the hashing on a shared hardware queue
   for (int k = 0; k < 2 && e == hipSuccess; ++k) {
     e = hipEventCreateWithFlags(&copied[k].e, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&hashed[k].e, hipEventDisableTiming);

@@ -143,6 +143,14 @@ struct efes_ctx {
 
 namespace efes {
 
+// A stream with a hardware queue of its own, for work that must run beside the process's other
+// streams: HIP spreads ALL of a process's streams over GPU_MAX_HW_QUEUES (4) queues, so two
+// ordinary streams may share one and serialize.  A stream created with a CU mask gets a queue of
+// its own (the mask is a queue property); the mask is every CU, so placement is unchanged.
+// EFES_PART_STREAMS=plain makes ordinary streams (A/B).  Used for the planned batch's part
+// streams and efes_hash_host's copy stream.
+hipError_t own_queue_stream(const efes_ctx* ctx, hipStream_t* out);
+
 // Kernel shape for jobs whose bytes are read over PCIe in place (pinned, device-mapped host
 // memory): the lowest-latency shape that keeps each job's reads long -- DEEP (4 KiB per job per
 // super-step), then grouped DEEP with as many lanes per job as fit (G*64 contiguous bytes);

@@ -232,6 +232,7 @@ void efes_ctx_destroy(efes_ctx* ctx) {
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     for (hipStream_t sd : ctx->side)
       if (sd) (void)hipStreamSynchronize(sd);
+    if (ctx->copy) (void)hipStreamSynchronize(ctx->copy);
     if (ctx->d_tabs) (void)hipFree(ctx->d_tabs);
     if (ctx->d_span) (void)hipFree(ctx->d_span);
     if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
@@ -239,6 +240,7 @@ void efes_ctx_destroy(efes_ctx* ctx) {
       if (ev) (void)hipEventDestroy(ev);
     for (hipStream_t sd : ctx->side)
       if (sd) (void)hipStreamDestroy(sd);
+    if (ctx->copy) (void)hipStreamDestroy(ctx->copy);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   }
   delete ctx;

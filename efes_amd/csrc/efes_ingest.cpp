@@ -41,13 +41,6 @@ struct PinnedBuf {  // pinned host allocation released on scope exit
   T* as() const { return static_cast<T*>(p); }
 };
 
-struct Stream {
-  hipStream_t s = nullptr;
-  ~Stream() {
-    if (s) (void)hipStreamDestroy(s);
-  }
-};
-
 struct Event {
   hipEvent_t e = nullptr;
   ~Event() {
@@ -200,9 +193,21 @@ int efes_hash_host(efes_ctx* ctx, const efes_job* jobs, uint32_t n, uint64_t seg
   if (e == hipSuccess) e = h_jobs.alloc(2 * sizeof(efes_job) * n);
   if (e != hipSuccess) return EFES_ERR_HIP;
 
-  Stream copy;
+  // The context's copy stream: a hardware queue of its own, so the copies never wait behind the
+  // hashing on a shared queue; made once per context (every CU-masked stream holds a queue, and
+  // the GPU's queue slots are few).  One efes_hash_host at a time per context uses it.
+  {
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (!ctx->copy && efes::own_queue_stream(ctx, &ctx->copy) != hipSuccess) ctx->copy = nullptr;
+    if (!ctx->copy) return EFES_ERR_HIP;
+  }
+  std::unique_lock<std::mutex> copy_lk(ctx->copy_mu);
+  struct CopyStream {  // drained on every exit, before the buffers above are freed
+    hipStream_t s;
+    ~CopyStream() { (void)hipStreamSynchronize(s); }
+  } copy{ctx->copy};
   Event copied[2], hashed[2];
-  e = efes::own_queue_stream(ctx, &copy.s);  // never behind the hashing on a shared hardware queue
+  e = hipSuccess;
   for (int k = 0; k < 2 && e == hipSuccess; ++k) {
     e = hipEventCreateWithFlags(&copied[k].e, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&hashed[k].e, hipEventDisableTiming);

@@ -136,8 +136,10 @@ struct efes_ctx {
   std::mutex plan_mu;             // one planned submit at a time uses the side streams/events
   efes::Tables* d_tabs = nullptr;
   efes::SpanTables* d_span = nullptr;  // operators of the span CRC (efes_crc32_span)
-  std::mutex mu;                  // guards the lazy creation of `digests`
+  std::mutex mu;                  // guards the lazy creation of `digests` and `copy`
   efes_queue* digests = nullptr;  // shared queue of the streaming digests (efes_stream.cpp)
+  hipStream_t copy = nullptr;     // efes_hash_host's H2D stream (own_queue_stream), created on first use
+  std::mutex copy_mu;             // one efes_hash_host at a time on `copy`
   efes::DigestRegistry dreg;      // the digests holding an upload of `digests`
 };
 

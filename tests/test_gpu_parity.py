@@ -231,6 +231,28 @@ def test_sha_only_and_crc_only(env, oracle, mode):
         assert bytes(b2.sums_host()[i][20:]) == zlib.crc32(d).to_bytes(4, "big")
 
 
+def test_wide_uniform_phase_sha_only_and_crc_only(env, oracle):
+    """WIDE's uniform loop (every lane of a wave has >= 5 blocks left: no per-lane selects) with one
+    of the two hashes only: 192 jobs of 8-24 KiB fill three whole waves, so the uniform phase runs
+    for SHA-1 alone and for the position-table CRC alone (efes_kernels.hip wide_bulk)."""
+    n = 192
+    rng = random.Random(77)
+    lengths = [8192 + 64 * rng.randint(0, 256) + rng.randint(0, 63) for _ in range(n)]
+    stride = 32768
+    host = oracle.fill_synthetic(stride * n, 19)
+    buf = device_buffer(env, host)
+    offs = [i * stride for i in range(n)]
+    wide = _modes(env)["wide"]
+    b1 = env["DeviceBatch"](buf.data_ptr(), offs, lengths, crc32=False, ctx=env["ctx"])
+    b1.run(wide)
+    b2 = env["DeviceBatch"](buf.data_ptr(), offs, lengths, sha1=False, ctx=env["ctx"])
+    b2.run(wide)
+    for i, (o, L) in enumerate(zip(offs, lengths)):
+        d = host[o:o + L].tobytes()
+        assert b1.sha1_hex()[i] == hashlib.sha1(d).hexdigest(), (i, L)
+        assert b2.crc_sum()[i] == zlib.crc32(d), (i, L)
+
+
 def test_zero_jobs(env):
     env["ctx"].submit(0, 0)
     env["ctx"].sync()
@@ -441,6 +463,40 @@ def test_host_ingest_matches_oracle(env, oracle, segment):
         d = host[o:o + L].tobytes()
         assert hb.sha1_hex()[i] == hashlib.sha1(d).hexdigest(), (segment, L)
         assert int(hb.crc_sum()[i]) == zlib.crc32(d), (segment, L)
+
+
+def test_host_ingest_concurrent_calls_one_context(env, oracle):
+    """Four threads in efes_hash_host on one context: they share its copy stream (one hardware
+    queue of its own, efes_ingest.cpp) one call at a time, and every digest stays right."""
+    import threading
+    from efes_amd.batch import HostBatch
+    results, errors = {}, []
+
+    def work(t):
+        try:
+            rng = random.Random(100 + t)
+            lengths = [rng.randint(0, 150000) for _ in range(17)] + [64 * (t + 1), 0]
+            offsets = np.concatenate([[0], np.cumsum(lengths)[:-1]]).astype(np.uint64).tolist()
+            host = oracle.fill_synthetic(sum(lengths) + 8, 900 + t)
+            hb = HostBatch(host.ctypes.data, offsets, lengths, ctx=env["ctx"])
+            hb.run(16384 * (t + 1))
+            results[t] = (host, offsets, lengths, hb.sha1_hex(), hb.crc_sum(), hb.status[: hb.n].copy())
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errors.append(repr(e))
+
+    threads = [threading.Thread(target=work, args=(t,)) for t in range(4)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join(timeout=100)
+    assert not errors, errors
+    assert sorted(results) == [0, 1, 2, 3]
+    for t, (host, offsets, lengths, sha, crc, status) in results.items():
+        assert (status == 0).all()
+        for i, (o, L) in enumerate(zip(offsets, lengths)):
+            d = host[o:o + L].tobytes()
+            assert sha[i] == hashlib.sha1(d).hexdigest(), (t, i, L)
+            assert int(crc[i]) == zlib.crc32(d), (t, i, L)
 
 
 def test_host_ingest_pinned_strided_and_resume(env, oracle):

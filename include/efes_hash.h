@@ -183,8 +183,9 @@ int efes_fill_synthetic(efes_ctx* ctx, void* dst_device, size_t bytes, uint64_t 
  * The reference's path starts in host memory (a socket buffer, filereceiver.go:208-209).
  * efes_hash_host runs the jobs of a HOST array whose data/sha1/crc32/sum/status pointers are
  * all HOST memory: segment s (segment_bytes, rounded up to 64; 0 = 256 KiB) of every message is
- * copied H2D with hipMemcpyAsync on a copy stream into one of two device slots while segment
- * s-1 is hashed on the context stream; states stay on the device between segments (the
+ * copied H2D with hipMemcpyAsync on the context's copy stream (a hardware queue of its own) into
+ * one of two device slots while segment s-1 is hashed on the context stream; concurrent calls on
+ * one context take the copy stream in turn; states stay on the device between segments (the
  * per-PATCH resume of filereceiver.go:182-226); states, sums and status are copied back at
  * the end.  Equivalent to one Write per segment (so the stale bytes x[nx:64] are those of
  * segment-sized Writes, sha1.go:75-77).  Messages whose host addresses advance by a constant stride are copied with one

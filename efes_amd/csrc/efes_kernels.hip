@@ -1712,7 +1712,8 @@ hipError_t launch_wide(const efes_job* jobs, uint32_t njobs, const Tables* tabs,
     }
     big_ok = st == 1;
   }
-  if (!big_ok && xs > 48 * 1024) return hipErrorInvalidConfiguration;
+  // without the raised limit a workgroup gets 64 KiB of LDS in all (static: the CRC tables)
+  if (!big_ok && sizeof(WideLDS) + xs > 64 * 1024) return hipErrorInvalidConfiguration;
   // exclusive: reserve the CU's whole LDS, so no other workgroup shares its SIMDs
   const size_t dyn = exclusive && big_ok ? kCuLds - static_lds : xs;
   hipLaunchKernelGGL(wide_kernel, dim3((njobs + per - 1) / per), dim3(per), dyn, s, jobs, njobs, tabs);

@@ -150,7 +150,9 @@ namespace efes {
 // ordinary streams may share one and serialize.  A stream created with a CU mask gets a queue of
 // its own (the mask is a queue property); the mask is every CU, so placement is unchanged.
 // EFES_PART_STREAMS=plain makes ordinary streams (A/B).  Used for the planned batch's part
-// streams and efes_hash_host's copy stream.
+// streams and efes_hash_host's copy stream.  HIP creates CU-masked streams as blocking streams
+// (hipStreamDefault): they also order against the legacy NULL stream, which adds ordering,
+// never removes it.
 hipError_t own_queue_stream(const efes_ctx* ctx, hipStream_t* out);
 
 // Kernel shape for jobs whose bytes are read over PCIe in place (pinned, device-mapped host

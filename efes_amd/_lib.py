@@ -82,7 +82,14 @@ class QueueStats(ctypes.Structure):
                 ("free_uploads", ctypes.c_uint32), ("max_uploads", ctypes.c_uint32)]
 
 
+class PairStats(ctypes.Structure):
+    """efes_pair_stats (ABI 6): process-wide counters of fused CRC + SHA-1 digest pairs."""
+    _fields_ = [("pairs", ctypes.c_uint64), ("fused_writes", ctypes.c_uint64), ("fused_bytes", ctypes.c_uint64),
+                ("settles", ctypes.c_uint64)]
+
+
 assert ctypes.sizeof(Sha1State) == 104 and ctypes.sizeof(Job) == 56 and ctypes.sizeof(QueueStats) == 32
+assert ctypes.sizeof(PairStats) == 32
 
 # numpy mirrors for building arrays of jobs / states in bulk
 JOB_DTYPE = np.dtype([("data", "<u8"), ("length", "<u8"), ("sha1", "<u8"), ("crc32", "<u8"), ("sum", "<u8"),
@@ -132,6 +139,8 @@ SIGNATURES = {
     "efes_sha1_new_zero_pool": (_I, [_VP, _P(_VP)]),
     "efes_crc32_new_pool": (_I, [_VP, _P(_VP)]),
     "efes_pool_stats": (_I, [_VP, _U32, _P(QueueStats)]),
+    "efes_pair_stats_get": (_I, [_P(PairStats)]),
+    "efes_debug_fault_after": (_I, [_VP, _U64]),
     "efes_sha1_new": (_I, [_VP, _P(_VP)]),
     "efes_sha1_new_zero": (_I, [_VP, _P(_VP)]),
     "efes_sha1_free": (None, [_VP]),

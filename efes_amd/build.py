@@ -58,6 +58,13 @@ def build_tools() -> list[str]:
                         "-L", LIB_DIR, "-lefeshash", "-Wl,-rpath,$ORIGIN/../efes_amd/lib", "-pthread"], check=True)
     if os.path.exists(exe):
         out.append(exe)
+    src = os.path.join(ROOT, "tools", "bench_go_surface.cpp")
+    exe = os.path.join(ROOT, "tools", "bench_go_surface")
+    if os.path.exists(src) and _stale(exe, [src, LIB, os.path.join(ROOT, "include", "efes_hash.h")]):
+        subprocess.run(["g++", "-O2", "-std=c++17", "-Wall", "-Wextra", "-pthread", "-I", os.path.join(ROOT, "include"),
+                        src, "-o", exe, "-L", LIB_DIR, "-lefeshash", "-Wl,-rpath,$ORIGIN/../efes_amd/lib"], check=True)
+    if os.path.exists(exe):
+        out.append(exe)
     src = os.path.join(ROOT, "tools", "bench_receiver.cpp")
     exe = os.path.join(ROOT, "tools", "bench_receiver")
     if os.path.exists(src) and _stale(exe, [src, RECEIVER_LIB, RECEIVER_HDR, LIB]):

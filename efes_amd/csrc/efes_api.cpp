@@ -199,10 +199,9 @@ int efes_ctx_create(int device, efes_ctx** out) {
   ctx->cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
   hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming);
-  // The part streams of a planned batch must land on distinct hardware queues, or parts meant to
-  // run side by side serialize (configs[3] in a fresh process: 1.03-1.09 s per step on ordinary
-  // streams, 0.885 s with 8 queues or CU-masked streams).
-  for (int i = 0; i < EFES_PLAN_MAX_PARTS && e == hipSuccess; ++i) e = efes::own_queue_stream(ctx, &ctx->side[i]);
+  // The part streams of a planned batch are created by the first multi-part efes_hash_submit_plan
+  // (efes_plan.cpp): each holds a hardware queue of its own, which a context that never plans
+  // should not take from the process.
   for (int i = 0; i < EFES_PLAN_MAX_PARTS && e == hipSuccess; ++i)
     e = hipEventCreateWithFlags(&ctx->ev_join[i], hipEventDisableTiming);
   if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&ctx->d_tabs), tab_bytes);

@@ -48,14 +48,45 @@ efes_queue* stream_queue(efes_ctx* ctx, int* rc);
 // digest layer can evict an idle digest and retry instead of failing (efes_queue.cpp).
 int upload_open_slot(efes_queue* q, uint32_t hashes, const efes_sha1_state* sha1, const efes_crc32_state* crc32,
                      efes_upload** out, bool* no_slot);
-uint32_t queue_free_slots(efes_queue* q);
+// Free upload slots of q, or -1 once q has latched a device fault (placement skips it).
+int64_t queue_free_slots(efes_queue* q);
+// Test hook behind efes_debug_fault_after: q's k-th launch from now reports a device fault.
+void queue_set_fault_after(efes_queue* q, uint64_t k);
+
+// ---- fused digest pairs (efes_stream.cpp on efes_queue.cpp) ----------------------------------
+// io.MultiWriter(f, CRC32, Sha1) (filereceiver.go:208) hands the same bytes to a CRC digest and
+// then to a SHA-1 digest; the digest layer binds such a pair to ONE upload that keeps both hashes.
+// The leader's (CRC) Write stages its bytes without handing them to the dispatcher; the follower's
+// (SHA-1) identical Write is checked against the staged bytes and confirms them.
+uint64_t upload_chunk_bytes(const efes_upload* u);
+// u holds exactly n staged bytes in its current chunk and nothing queued or running (its first Write).
+bool upload_holds_only(efes_upload* u, size_t n);
+// Host address of byte `off` of u's current staging chunk.
+const uint8_t* upload_staged(const efes_upload* u, uint64_t off);
+// u now keeps SHA-1 too: its device SHA-1 state starts from `sha`, the host replay from `shadow`.
+void upload_fuse(efes_upload* u, const efes_sha1_state& sha, const efes_sha1_state& shadow);
+// u keeps only `hashes` from now on (a member of a fused pair left it).
+void upload_keep(efes_upload* u, uint32_t hashes);
+// Stages n <= chunk bytes into u's current chunk WITHOUT handing them over (a current chunk without
+// room is handed over first); *off = their offset in the current chunk.  No host replay.
+int upload_stage(efes_upload* u, const void* p, size_t n, uint64_t* off);
+// The follower matched the staged bytes: its replayed Go state; a full chunk is handed over.
+int upload_confirm(efes_upload* u, const efes_sha1_state& shadow);
+// Drops the staged bytes of the current chunk from offset `off` on (never handed over).
+void upload_truncate(efes_upload* u, uint64_t off);
 
 // Streaming digests (efes_stream.cpp) that hold an upload of a context's digest queue, oldest
-// first: the candidates for eviction when a digest needs a state slot and none is free.
+// first: the candidates for eviction when a digest needs a state slot and none is free.  An
+// entry is a digest holding an upload alone, or a fused pair holding one for both members.
 struct Digest;
+struct Fused;
+struct OpenRef {
+  Digest* d;
+  Fused* f;
+};
 struct DigestRegistry {
   std::mutex mu;
-  std::list<Digest*> open;
+  std::list<OpenRef> open;
   std::condition_variable released;  // a digest gave its upload back
 };
 
@@ -141,6 +172,7 @@ struct efes_ctx {
   hipStream_t copy = nullptr;     // efes_hash_host's H2D stream (own_queue_stream), created on first use
   std::mutex copy_mu;             // one efes_hash_host at a time on `copy`
   efes::DigestRegistry dreg;      // the digests holding an upload of `digests`
+  uint64_t fault_after = 0;       // test hook (efes_debug_fault_after): the digest queue's k-th launch faults
 };
 
 namespace efes {

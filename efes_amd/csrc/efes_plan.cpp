@@ -388,6 +388,16 @@ int efes_hash_submit_plan(efes_ctx* ctx, const efes_job* jobs, const efes_plan* 
   // round-robin over every stream of the process, so distinct queues are likely -- the part
   // streams are created one after the other -- but not guaranteed.
   if (plan->nparts == 1) return hip_err_plan(launch(plan->part[0], jobs, s));
+  // The part streams, created on the first multi-part plan (plan_mu held).  They must land on
+  // distinct hardware queues, or parts meant to run side by side serialize (configs[3] in a fresh
+  // process: 1.03-1.09 s per step on ordinary streams, 0.885 s on CU-masked streams, which get a
+  // queue each).  A driver that refuses CU masking still gets ordinary streams.
+  for (int i = 0; i < EFES_PLAN_MAX_PARTS; ++i)
+    if (!ctx->side[i] && efes::own_queue_stream(ctx, &ctx->side[i]) != hipSuccess &&
+        hipStreamCreateWithFlags(&ctx->side[i], hipStreamNonBlocking) != hipSuccess) {
+      ctx->side[i] = nullptr;
+      return EFES_ERR_HIP;
+    }
   hipError_t e = hipEventRecord(ctx->ev_fork, s);
   const efes_job* first = jobs;
   for (uint32_t i = 0; i < plan->nparts && e == hipSuccess; ++i) {

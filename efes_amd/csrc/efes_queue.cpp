@@ -95,7 +95,7 @@ struct efes_queue {
   bool stop = false;
   int fault = EFES_OK;
   uint64_t n_launches = 0, n_jobs = 0, n_bytes = 0;  // efes_queue_get_stats
-  uint64_t n_attempts = 0, inject_at = 0;  // test hook: EFES_FAULT_INJECT_LAUNCH=k fails launch k
+  uint64_t n_attempts = 0, inject_at = 0;  // test hook (efes_debug_fault_after): launch k faults
   // hipEventBlockingSync: the dispatcher sleeps in retire instead of polling the event, so it does
   // not keep a host core busy beside the request threads (receiver within noise either way:
   // profiles/r03_receiver/ab_sync_*.log); EFES_QUEUE_SYNC=spin restores the poll.
@@ -181,6 +181,8 @@ void efes_queue::run() {
       j.flags = sum ? EFES_JOB_FINALIZE | EFES_JOB_SUM_ONLY : fold ? EFES_JOB_FINALIZE : 0u;
       j._reserved = 0;
     }
+    // test hook (efes_debug_fault_after): this launch reports a device fault instead of running
+    const bool inject = inject_at && ++n_attempts == inject_at;
     lk.unlock();  // callers keep staging while this batch is copied and launched
     // No H2D copy of the data: the DEEP kernel reads the pinned chunks in place (4 KiB per
     // wave per super-step, prefetched a super-step ahead, so the PCIe latency is hidden behind
@@ -190,7 +192,7 @@ void efes_queue::run() {
     // DEEP (or grouped DEEP beyond one chunk per SIMD): efes::pcie_mode.
     const uint32_t nb = (uint32_t)b.items.size();
     int rc = e == hipSuccess ? EFES_OK : EFES_ERR_HIP;
-    if (rc == EFES_OK && inject_at && ++n_attempts == inject_at) rc = EFES_ERR_DEVICE_FAULT;  // as a faulted kernel
+    if (rc == EFES_OK && inject) rc = EFES_ERR_DEVICE_FAULT;  // as a faulted kernel
     if (rc == EFES_OK) rc = efes_hash_submit_mode(ctx, dj, nb, stream, efes::pcie_mode(ctx, nb));
     if (rc == EFES_OK && hipEventCreateWithFlags(&b.ev, ev_flags) != hipSuccess) rc = EFES_ERR_HIP;
     if (rc == EFES_OK && hipEventRecord(b.ev, stream) != hipSuccess) rc = EFES_ERR_HIP;
@@ -311,9 +313,6 @@ int efes_queue_create(efes_ctx* ctx, uint64_t chunk_bytes, uint32_t max_chunks, 
   q->max_uploads = max_uploads;
   const char* ah = getenv("EFES_QUEUE_AHEAD");
   q->ahead = ah && *ah ? strtoull(ah, nullptr, 10) : kAhead;
-  // Test hook (tests/test_gpu_boundary.py): the k-th launch of every queue created while it is set
-  // reports a device fault instead of running, as a kernel that faulted would.
-  if (const char* fi = getenv("EFES_FAULT_INJECT_LAUNCH")) q->inject_at = strtoull(fi, nullptr, 10);
   if (const char* qs = getenv("EFES_QUEUE_SYNC"); qs && !strcmp(qs, "spin")) q->ev_flags = hipEventDisableTiming;
   DeviceGuard g(ctx->device);
   hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&q->h_slab), q->chunk * max_chunks, hipHostMallocMapped);
@@ -367,6 +366,18 @@ int efes_upload_open(efes_queue* q, uint32_t hashes, const efes_sha1_state* sha1
   return efes::upload_open_slot(q, hashes, sha1, crc, out, &no_slot);
 }
 
+int efes_debug_fault_after(efes_ctx* ctx, uint64_t k) {
+  if (!ctx) return EFES_ERR_ARG;
+  efes_queue* q;
+  {
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->fault_after = k;  // for the digest queue if it is created later (efes_stream.cpp)
+    q = ctx->digests;
+  }
+  if (q) efes::queue_set_fault_after(q, k);
+  return EFES_OK;
+}
+
 int efes_queue_get_stats(efes_queue* q, efes_queue_stats* out) {
   if (!q || !out) return EFES_ERR_ARG;
   std::lock_guard<std::mutex> lk(q->mu);
@@ -380,9 +391,15 @@ int efes_queue_get_stats(efes_queue* q, efes_queue_stats* out) {
 
 }  // extern "C"
 
-uint32_t efes::queue_free_slots(efes_queue* q) {
+int64_t efes::queue_free_slots(efes_queue* q) {
   std::lock_guard<std::mutex> lk(q->mu);
-  return (uint32_t)q->free_states.size();
+  return q->fault ? -1 : (int64_t)q->free_states.size();
+}
+
+void efes::queue_set_fault_after(efes_queue* q, uint64_t k) {
+  std::lock_guard<std::mutex> lk(q->mu);
+  q->inject_at = k;
+  q->n_attempts = 0;
 }
 
 int efes::upload_open_slot(efes_queue* q, uint32_t hashes, const efes_sha1_state* sha1, const efes_crc32_state* crc,
@@ -567,6 +584,70 @@ int efes_upload_sum(efes_upload* u, uint8_t out[24]) {
 
 namespace efes {
 efes_sha1_state upload_shadow(const efes_upload* u) { return u->shadow; }
+
+// ---- fused digest pairs (efes_internal.hpp; used by efes_stream.cpp) ----------------------------
+// The caller owns the upload as its writer (cur/fill need no lock, as in efes_upload_write).
+uint64_t upload_chunk_bytes(const efes_upload* u) { return u->q->chunk; }
+
+bool upload_holds_only(efes_upload* u, size_t n) {
+  std::lock_guard<std::mutex> lk(u->q->mu);
+  return !u->latched && u->inflight == 0 && u->queued == 0 && u->cur >= 0 && u->fill == n && !u->fold_sum;
+}
+
+const uint8_t* upload_staged(const efes_upload* u, uint64_t off) {
+  return u->q->h_slab + (size_t)u->cur * u->q->chunk + off;
+}
+
+void upload_fuse(efes_upload* u, const efes_sha1_state& sha, const efes_sha1_state& shadow) {
+  std::lock_guard<std::mutex> lk(u->q->mu);  // the dispatcher reads `hashes` when it assembles a batch
+  u->hashes = EFES_HASH_SHA1 | EFES_HASH_CRC32;
+  // no job of u is queued or running (upload_holds_only): the slot is ours to write
+  memcpy(u->q->h_states + (size_t)u->dslot * kDevStateBytes, &sha, sizeof sha);
+  u->shadow = shadow;
+}
+
+void upload_keep(efes_upload* u, uint32_t hashes) {
+  std::lock_guard<std::mutex> lk(u->q->mu);
+  u->hashes = hashes;
+  if (!(hashes & EFES_HASH_SHA1)) {  // a CRC-only upload replays a NewSha1 state (never a panic state)
+    memset(&u->shadow, 0, sizeof u->shadow);
+    efes_sha1_state_init(&u->shadow);
+  }
+}
+
+int upload_stage(efes_upload* u, const void* p, size_t n, uint64_t* off) {
+  if (u->latched) return u->latched;
+  efes_queue* q = u->q;
+  if (u->cur >= 0 && u->fill + n > q->chunk) {  // no room: hand the (matched) chunk over first
+    std::unique_lock<std::mutex> lk(q->mu);
+    enqueue_current(u, lk);
+    pace(u, lk);
+  }
+  if (u->cur < 0) {
+    std::unique_lock<std::mutex> lk(q->mu);
+    if (int rc = take_chunk(u, lk)) return rc;
+    u->fill = 0;
+  }
+  copy_to_staging(q->h_slab + (size_t)u->cur * q->chunk + u->fill, static_cast<const uint8_t*>(p), n);
+  *off = u->fill;
+  u->fill += n;
+  return EFES_OK;
+}
+
+int upload_confirm(efes_upload* u, const efes_sha1_state& shadow) {
+  u->shadow = shadow;
+  efes_queue* q = u->q;
+  if (u->cur >= 0 && u->fill == q->chunk) {
+    std::unique_lock<std::mutex> lk(q->mu);
+    enqueue_current(u, lk);
+    pace(u, lk);
+  }
+  return u->latched;
+}
+
+void upload_truncate(efes_upload* u, uint64_t off) {
+  if (u->cur >= 0 && off < u->fill) u->fill = off;
+}
 }  // namespace efes
 
 extern "C" {

@@ -3,10 +3,10 @@
 //
 // sha1digest (sha1.go:29-120, sha1_efes.go:25-64) and crc32digest (crc32.go:48-93,
 // crc32_efes.go:18-40) keep their method sets; each object is an efes_upload of a context's
-// shared digest queue that keeps only its own hash (EFES_HASH_SHA1 or EFES_HASH_CRC32).  So the Go
-// code of filereceiver.go -- io.MultiWriter(f, CRC32, Sha1) in every request goroutine --
-// drops in unchanged and still gets batched launches across all concurrent requests: a Write
-// stages into pinned memory and returns; Sum / MarshalText are the sync points.
+// shared digest queue.  So the Go code of filereceiver.go -- io.MultiWriter(f, CRC32, Sha1) in
+// every request goroutine -- drops in unchanged and still gets batched launches across all
+// concurrent requests: a Write stages into pinned memory and returns; Sum / MarshalText are the
+// sync points.
 //
 // Go's Write never fails, and the Go code frees digests only through the garbage collector, so an
 // upload slot is held only while it is needed (efes_hash.h, layer 2):
@@ -19,8 +19,27 @@
 // Every call holds the digest's mutex (one goroutine per digest, so it is uncontended), which is
 // what lets another thread evict the digest safely between calls.
 //
+// FUSED PAIRS (round 4).  MultiWriter(f, CRC32, Sha1) (filereceiver.go:208-209, fileinfo.go:20-27)
+// hands every body buffer p to the CRC digest and then, unchanged, to the SHA-1 digest.  Two
+// separate uploads would stage p twice and launch two jobs that each read it over PCIe.  Instead:
+//   * a CRC digest whose Write opened a fresh upload registers that Write (p, n) as a candidate;
+//   * a parked SHA-1 digest whose Write has the same (p, n) BINDS to it if the candidate's staged
+//     bytes equal p (memcmp): the upload then keeps both hashes, the SHA-1 state slot starts from
+//     the SHA-1 digest's parked state, and nothing is staged for the SHA-1 Write;
+//   * after that the leader's (CRC) Write stages its bytes but does not hand them to the
+//     dispatcher; the follower's (SHA-1) Write of the same (p, n) is checked against them (memcmp)
+//     and confirms them -- one staging copy and one fused job per body byte;
+//   * anything else -- a Write to one digest only, different bytes, a Sum / MarshalText of the
+//     leader first, Reset / UnmarshalText / free of one, an eviction -- SETTLES the pair: every
+//     confirmed byte is hashed into both states, the leader's unconfirmed bytes into its state
+//     only, and both digests continue alone (a follower's sync point or a member whose state is
+//     being replaced just LEAVES, the partner keeping the upload).
+// So a wrong guess costs time, never correctness: every digest hashes exactly the bytes of its
+// own Writes, in order.  EFES_DIGEST_FUSE=0 disables binding (A/B).
+//
 // Placement: a digest made on a context uses that context's queue; one made on a pool
-// (efes_pool_create) opens each upload on the pool's context with the most free slots.
+// (efes_pool_create) opens each upload on the pool's context with the most free slots, skipping
+// contexts whose queue has latched a device fault.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -29,6 +48,7 @@
 #include <atomic>
 #include <chrono>
 #include <new>
+#include <unordered_map>
 #include <vector>
 
 #include "efes_internal.hpp"
@@ -46,12 +66,37 @@ struct Digest {
   efes_pool* pool = nullptr;   // a context chosen at every (re)open
   uint32_t hashes = 0;         // EFES_HASH_SHA1 or EFES_HASH_CRC32
   efes_ctx* on = nullptr;      // the context whose digest queue holds `u`
-  efes_upload* u = nullptr;    // null while parked
-  std::list<Digest*>::iterator pos;  // in on->dreg.open while u != nullptr
+  efes_upload* u = nullptr;    // null while parked (and while fused: the pair holds the upload)
+  std::list<OpenRef>::iterator pos;  // in on->dreg.open while u != nullptr
   efes_sha1_state sbase{};     // the parked state (sha1digest)
   efes_crc32_state cbase{};    // the parked state (crc32digest)
   int latched = EFES_OK;       // an error the next sync point reports (Go would have panicked, or a fault)
+  Fused* fz = nullptr;         // the fused pair this digest is a member of (u/on unused meanwhile)
+  const void* cand_p = nullptr;  // a CRC digest whose upload holds exactly its first Write (cand_p, cand_n)
+  size_t cand_n = 0;
   bool sha() const { return hashes == EFES_HASH_SHA1; }
+  virtual ~Digest() = default;
+};
+
+// One upload shared by a CRC digest (the leader: MultiWriter writes it first) and a SHA-1 digest
+// (the follower).  Guarded by `mu`, taken after the member's own mutex.
+struct Fused {
+  std::mutex mu;
+  efes_upload* u = nullptr;        // null once settled
+  efes_ctx* on = nullptr;
+  std::list<OpenRef>::iterator pos;  // in on->dreg.open while u != nullptr
+  bool lead_in = true, follow_in = true;  // members still sharing the upload
+  int refs = 2;                    // members whose fz still points here
+  // the leader's last Write: staged in u's current chunk, not yet matched by the follower
+  bool open = false;
+  const void* op = nullptr;
+  size_t on_bytes = 0;
+  uint64_t ooff = 0;
+  // after settle(): both states after every byte, for the members to pick up at their next call
+  bool settled = false;
+  efes_sha1_state sha_out{};
+  efes_crc32_state crc_out{};
+  int rc_sha = EFES_OK, rc_crc = EFES_OK;
 };
 
 }  // namespace efes
@@ -60,8 +105,21 @@ struct efes_sha1 : efes::Digest {};
 struct efes_crc32 : efes::Digest {};
 
 using efes::Digest;
+using efes::Fused;
+using efes::OpenRef;
 
 namespace {
+
+// Process-wide counters (efes_pair_stats_get).
+std::atomic<uint64_t> g_pairs{0}, g_fused_writes{0}, g_fused_bytes{0}, g_settles{0};
+
+bool fuse_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("EFES_DIGEST_FUSE");
+    return !(e && !strcmp(e, "0"));
+  }();
+  return on;
+}
 
 // Shared queue sizing: EFES_DIGEST_STAGING_MIB of pinned staging (default 256 MiB) in chunks of
 // EFES_DIGEST_CHUNK_KIB (default 64 KiB: 4096 chunks, so up to 4095 digests hold an upload at once).
@@ -75,7 +133,39 @@ efes_queue* create_digest_queue(efes_ctx* ctx, int* rc) {
   const uint32_t chunks = (uint32_t)((mib << 20) / chunk) < 16 ? 16u : (uint32_t)((mib << 20) / chunk);
   efes_queue* q = nullptr;
   *rc = efes_queue_create(ctx, chunk, chunks, chunks - 1, &q);
+  if (*rc == EFES_OK && ctx->fault_after) efes::queue_set_fault_after(q, ctx->fault_after);
   return *rc == EFES_OK ? q : nullptr;
+}
+
+// ---- leader candidates: CRC digests whose fresh upload holds exactly one Write (p, n) -----------
+struct CandShard {
+  std::mutex mu;
+  std::unordered_map<const void*, Digest*> m;
+};
+CandShard g_cand[64];
+
+CandShard& shard_of(const void* p) {
+  const uint64_t h = (uint64_t)reinterpret_cast<uintptr_t>(p) * 0x9E3779B97F4A7C15ull;
+  return g_cand[h >> 58];
+}
+
+void uncandidate(Digest* d) {  // d->mu held
+  if (!d->cand_p) return;
+  CandShard& s = shard_of(d->cand_p);
+  {
+    std::lock_guard<std::mutex> lk(s.mu);
+    auto it = s.m.find(d->cand_p);
+    if (it != s.m.end() && it->second == d) s.m.erase(it);
+  }
+  d->cand_p = nullptr;
+}
+
+void candidate(Digest* d, const void* p, size_t n) {  // d->mu held
+  CandShard& s = shard_of(p);
+  std::lock_guard<std::mutex> lk(s.mu);
+  s.m[p] = d;
+  d->cand_p = p;
+  d->cand_n = n;
 }
 
 }  // namespace
@@ -89,21 +179,21 @@ efes_queue* efes::stream_queue(efes_ctx* ctx, int* rc) {
 
 namespace {
 
-void unlist(Digest* d) {  // d->mu held, d->u open
-  efes::DigestRegistry& r = d->on->dreg;
+void unlist(efes_ctx* on, std::list<OpenRef>::iterator pos) {
+  efes::DigestRegistry& r = on->dreg;
   {
     std::lock_guard<std::mutex> lk(r.mu);
-    r.open.erase(d->pos);
+    r.open.erase(pos);
   }
   r.released.notify_all();
 }
 
 // Gives the upload back, dropping bytes staged since the last sync point (the state is being
-// replaced: UnmarshalText, Reset, free).  d->mu held.
+// replaced: UnmarshalText, Reset, free).  d->mu held, d not fused.
 void drop(Digest* d) {
   if (!d->u) return;
   efes_upload* u = d->u;
-  unlist(d);
+  unlist(d->on, d->pos);
   d->u = nullptr;
   d->on = nullptr;
   efes_upload_close(u);
@@ -111,7 +201,7 @@ void drop(Digest* d) {
 
 // Parks the digest: the state after every staged byte (h / crc from the device, Go's x/nx/len
 // replayed on the host) moves to sbase / cbase and the upload is given back.  A failure is
-// latched for the next sync point.  d->mu held.
+// latched for the next sync point.  d->mu held, d not fused.
 void park(Digest* d) {
   if (!d->u) return;
   efes_sha1_state s = efes::upload_shadow(d->u);  // x/nx/len (Reset keeps x even after a failure)
@@ -123,21 +213,175 @@ void park(Digest* d) {
   drop(d);
 }
 
-// Evicts the oldest digest of ctx's queue that is not inside a call (and is not `self`).
+// ---- fused pairs --------------------------------------------------------------------------------
+// Settles the pair (z->mu held): every matched byte is hashed into both states, the leader's
+// unmatched Write (if any) into the CRC state alone; both states are left for the members to pick
+// up and the upload is given back.
+void settle(Fused* z) {
+  efes_upload* u = z->u;
+  if (!u) return;
+  std::vector<uint8_t> tail;
+  if (z->open) {  // the leader's bytes the follower never matched: hashed for the leader only
+    const uint8_t* t = efes::upload_staged(u, z->ooff);
+    tail.assign(t, t + z->on_bytes);
+    efes::upload_truncate(u, z->ooff);
+    z->open = false;
+  }
+  efes_sha1_state s = efes::upload_shadow(u);
+  efes_crc32_state c{};
+  const int rc = efes_upload_state(u, &s, &c);  // waits for every matched byte (both hashes)
+  z->sha_out = s;
+  z->rc_sha = rc;
+  z->crc_out = c;
+  z->rc_crc = rc;
+  if (!tail.empty() && rc == EFES_OK && z->lead_in) {
+    efes::upload_keep(u, EFES_HASH_CRC32);
+    int rc2 = efes_upload_write(u, tail.data(), tail.size());
+    if (rc2 == EFES_OK) rc2 = efes_upload_state(u, nullptr, &c);
+    z->crc_out = c;
+    z->rc_crc = rc2;
+  }
+  unlist(z->on, z->pos);
+  efes_upload_close(u);
+  z->u = nullptr;
+  z->on = nullptr;
+  z->settled = true;
+  g_settles.fetch_add(1, std::memory_order_relaxed);
+}
+
+// d stops being a member of z (z->mu held through zk, released here); the last member frees z.
+void detach(Digest* d, Fused* z, std::unique_lock<std::mutex>& zk) {
+  d->fz = nullptr;
+  const bool last = --z->refs == 0;
+  zk.unlock();
+  if (last) delete z;
+}
+
+// d takes its state from a settled pair (park's conventions for failures).
+void pickup(Digest* d, const Fused* z) {
+  if (d->sha()) {
+    d->sbase = z->sha_out;
+    if (z->rc_sha != EFES_OK && d->latched == EFES_OK) d->latched = z->rc_sha;
+  } else if (z->rc_crc == EFES_OK) {
+    d->cbase = z->crc_out;
+  } else if (d->latched == EFES_OK) {
+    d->latched = z->rc_crc;
+  }
+}
+
+// The partner left: d holds the upload alone from now on (its hashes are d's already).
+void adopt(Digest* d, Fused* z) {
+  d->u = z->u;
+  d->on = z->on;
+  d->pos = z->pos;
+  {
+    std::lock_guard<std::mutex> lk(d->on->dreg.mu);
+    *d->pos = OpenRef{d, nullptr};
+  }
+  z->u = nullptr;
+  z->on = nullptr;
+}
+
+// d gives its share of the pair up and the partner keeps the upload (taking it over at its next
+// call).  sync: d's state after every matched byte is read first (d's sync point; the caller has
+// checked that no leader Write is unmatched); else d's state is being replaced and the leader's
+// unmatched bytes, if d is the leader, are dropped.  Returns the state read's error.
+int leave(Digest* d, Fused* z, bool sync, std::unique_lock<std::mutex>& zk) {
+  efes_upload* u = z->u;
+  int rc = EFES_OK;
+  if (d->sha()) {
+    if (sync) {
+      efes_sha1_state s = efes::upload_shadow(u);
+      rc = efes_upload_state(u, &s, nullptr);
+      d->sbase = s;
+      if (rc != EFES_OK && d->latched == EFES_OK) d->latched = rc;
+    }
+    efes::upload_keep(u, EFES_HASH_CRC32);
+    z->follow_in = false;
+  } else {
+    if (z->open) {
+      efes::upload_truncate(u, z->ooff);
+      z->open = false;
+    }
+    if (sync) {
+      efes_crc32_state c{};
+      rc = efes_upload_state(u, nullptr, &c);
+      if (rc == EFES_OK) d->cbase = c;
+      else if (d->latched == EFES_OK) d->latched = rc;
+    }
+    efes::upload_keep(u, EFES_HASH_SHA1);
+    z->lead_in = false;
+  }
+  detach(d, z, zk);
+  return rc;
+}
+
+// One call on a digest: d->mu, and for a member of a live pair the pair's mutex too (`z` set).  A
+// member of a settled pair picks up its state, one whose partner left takes the upload over; both
+// are alone again (`z` null).  A CRC digest's candidacy ends with its next call.
+struct Call {
+  Digest* d;
+  Fused* z = nullptr;
+  std::unique_lock<std::mutex> lk, zk;
+  explicit Call(Digest* dd) : d(dd), lk(dd->mu) {
+    uncandidate(d);
+    Fused* f = d->fz;
+    if (!f) return;
+    zk = std::unique_lock<std::mutex>(f->mu);
+    if (f->settled) {
+      pickup(d, f);
+      detach(d, f, zk);
+    } else if (!(d->sha() ? f->lead_in : f->follow_in)) {
+      adopt(d, f);
+      detach(d, f, zk);
+    } else {
+      z = f;
+    }
+  }
+  // the pair cannot go on for this call: settle it and continue alone
+  void split() {
+    settle(z);
+    pickup(d, z);
+    Fused* f = z;
+    z = nullptr;
+    detach(d, f, zk);
+  }
+  int leave(bool sync) {
+    Fused* f = z;
+    z = nullptr;
+    return ::leave(d, f, sync, zk);
+  }
+};
+
+// Evicts the oldest digest (or fused pair) of ctx's queue that is not inside a call (and is not `self`).
 bool evict_one(efes_ctx* ctx, Digest* self) {
   Digest* victim = nullptr;
+  Fused* pair = nullptr;
   {
     std::lock_guard<std::mutex> lk(ctx->dreg.mu);
-    for (Digest* d : ctx->dreg.open)
-      if (d != self && d->mu.try_lock()) {
-        victim = d;
+    for (const OpenRef& r : ctx->dreg.open) {
+      if (r.d) {
+        if (r.d != self && r.d->mu.try_lock()) {
+          victim = r.d;
+          break;
+        }
+      } else if (r.f->mu.try_lock()) {  // no member is inside an operation on the pair
+        pair = r.f;
         break;
       }
+    }
   }
-  if (!victim) return false;
-  park(victim);
-  victim->mu.unlock();
-  return true;
+  if (victim) {
+    park(victim);
+    victim->mu.unlock();
+    return true;
+  }
+  if (pair) {
+    settle(pair);  // the members pick their states up at their next calls
+    pair->mu.unlock();
+    return true;
+  }
+  return false;
 }
 
 efes_ctx* place(Digest* d) {
@@ -151,13 +395,20 @@ efes_ctx* place(Digest* d) {
     int rc = EFES_OK;
     efes_queue* q = efes::stream_queue(c, &rc);
     if (!q) continue;
-    const int64_t f = efes::queue_free_slots(q);
+    const int64_t f = efes::queue_free_slots(q);  // -1: the queue latched a device fault
     if (f > most) {
       most = f;
       best = c;
     }
   }
-  return best ? best : cs[start % n];
+  return best ? best : cs[start % n];  // every queue faulted: the sync point reports it
+}
+
+bool placed_on(const Digest* d, const efes_ctx* c) {
+  if (!d->pool) return c == d->home;
+  for (const efes_ctx* x : d->pool->ctxs)
+    if (x == c) return true;
+  return false;
 }
 
 // An upload holding the parked state; evicts or waits while the chosen queue is full.  d->mu held.
@@ -175,7 +426,7 @@ int acquire(Digest* d) {
     if (rc == EFES_OK) {
       d->on = c;
       std::lock_guard<std::mutex> lk(c->dreg.mu);
-      d->pos = c->dreg.open.insert(c->dreg.open.end(), d);
+      d->pos = c->dreg.open.insert(c->dreg.open.end(), OpenRef{d, nullptr});
       return EFES_OK;
     }
     if (!no_slot) return rc;
@@ -188,15 +439,95 @@ int acquire(Digest* d) {
   }
 }
 
+// A parked SHA-1 digest's Write (p, n) joins the CRC digest whose fresh upload holds exactly the
+// same bytes (MultiWriter(f, CRC32, Sha1) just wrote them there): the upload keeps both hashes
+// from now on.  f->mu held, f parked and not fused.
+bool try_bind(Digest* f, const void* p, size_t n) {
+  Digest* l;
+  {
+    CandShard& s = shard_of(p);
+    std::lock_guard<std::mutex> lk(s.mu);
+    auto it = s.m.find(p);
+    if (it == s.m.end()) return false;
+    l = it->second;
+    // try_lock: l's owner may be inside a call (or freeing l, which first takes l->mu and then
+    // this shard's lock): then no bind.  Holding the shard lock keeps l alive until we hold l->mu.
+    if (l == f || l->cand_n != n || !l->mu.try_lock()) return false;
+    s.m.erase(it);
+    l->cand_p = nullptr;
+  }
+  std::unique_lock<std::mutex> llk(l->mu, std::adopt_lock);
+  if (l->fz || !l->u || l->latched || l->sha() || !placed_on(f, l->on)) return false;
+  efes_upload* u = l->u;
+  if (!efes::upload_holds_only(u, n)) return false;
+  if (memcmp(efes::upload_staged(u, 0), p, n) != 0) return false;  // the staged bytes ARE this Write
+  efes_sha1_state shadow = f->sbase;
+  if (efes::replay_write(&shadow, static_cast<const uint8_t*>(p), n) != EFES_OK) return false;  // Go panics: alone
+  Fused* z = new (std::nothrow) Fused;
+  if (!z) return false;
+  efes::upload_fuse(u, f->sbase, shadow);
+  z->u = u;
+  z->on = l->on;
+  z->pos = l->pos;
+  {
+    std::lock_guard<std::mutex> lk(l->on->dreg.mu);
+    *z->pos = OpenRef{nullptr, z};
+  }
+  l->u = nullptr;
+  l->on = nullptr;
+  l->fz = z;
+  f->fz = z;
+  g_pairs.fetch_add(1, std::memory_order_relaxed);
+  g_fused_writes.fetch_add(1, std::memory_order_relaxed);
+  g_fused_bytes.fetch_add(n, std::memory_order_relaxed);
+  return true;
+}
+
 // Write(p): Go's never fails except where it panics (nx > 64 -> EFES_ERR_STATE).  Other errors
 // are latched for the next sync point.
 int digest_write(Digest* d, const void* p, size_t n) {
   if (!d || (!p && n)) return EFES_ERR_ARG;
-  std::lock_guard<std::mutex> lk(d->mu);
+  Call c(d);
+  if (Fused* z = c.z) {
+    efes_upload* u = z->u;
+    if (d->sha()) {  // the follower: the leader's Write of the same bytes is staged already
+      if (n == 0) {
+        if (efes::upload_shadow(u).nx != 64) return EFES_OK;  // an empty Write changes nothing
+      } else if (z->open && p == z->op && n == z->on_bytes &&
+                 memcmp(efes::upload_staged(u, z->ooff), p, n) == 0) {
+        efes_sha1_state sh = efes::upload_shadow(u);
+        if (efes::replay_write(&sh, static_cast<const uint8_t*>(p), n) == EFES_OK) {
+          z->open = false;
+          (void)efes::upload_confirm(u, sh);  // a fault is latched in the upload for the sync points
+          g_fused_writes.fetch_add(1, std::memory_order_relaxed);
+          g_fused_bytes.fetch_add(n, std::memory_order_relaxed);
+          return EFES_OK;
+        }
+      }
+    } else {  // the leader: stage, and wait for the follower's Write to match
+      if (n == 0) return EFES_OK;  // crc32.go:76-86 of nothing
+      if (!z->open && n <= efes::upload_chunk_bytes(u)) {
+        uint64_t off = 0;
+        if (efes::upload_stage(u, p, n, &off) == EFES_OK) {
+          z->open = true;
+          z->op = p;
+          z->on_bytes = n;
+          z->ooff = off;
+        }  // else the fault is latched in the upload
+        return EFES_OK;
+      }
+    }
+    c.split();  // the Writes diverged: both continue alone
+  }
   if (d->latched) return d->latched == EFES_ERR_STATE ? EFES_ERR_STATE : EFES_OK;
+  if (d->sha() && !d->u && n > 0 && fuse_enabled() && try_bind(d, p, n)) return EFES_OK;
+  const bool fresh = !d->u;
   int rc = acquire(d);
   if (rc == EFES_OK) rc = efes_upload_write(d->u, p, n);
-  if (rc == EFES_OK) return EFES_OK;
+  if (rc == EFES_OK) {
+    if (!d->sha() && fresh && n > 0 && fuse_enabled() && efes::upload_holds_only(d->u, n)) candidate(d, p, n);
+    return EFES_OK;
+  }
   d->latched = rc;
   return rc == EFES_ERR_STATE ? EFES_ERR_STATE : EFES_OK;
 }
@@ -230,20 +561,40 @@ int crc32_alloc(efes_ctx* ctx, efes_pool* pool, efes_crc32** out) {
   return EFES_OK;
 }
 
-void digest_free(Digest* d) {
+template <class D>
+void digest_free(D* d) {
   if (!d) return;
   {
-    std::lock_guard<std::mutex> lk(d->mu);
+    Call c(d);
+    if (c.z) c.leave(false);
     drop(d);
   }
   delete d;
 }
 
 // The full Go state now (h from the device after every staged byte, x/nx/len replayed); parks.
-int sha1_state_now(efes_sha1* d, efes_sha1_state* out) {  // d->mu held
+int sha1_state_now(Call& c, efes_sha1_state* out) {
+  efes_sha1* d = static_cast<efes_sha1*>(c.d);
+  if (c.z) {
+    if (c.z->open) c.split();
+    else c.leave(true);  // the matched bytes are all of this digest's bytes
+  }
   park(d);
   if (d->latched) return d->latched;
   *out = d->sbase;
+  return EFES_OK;
+}
+
+// The CRC's parked value after every byte written (sync point of Sum32 / Sum / MarshalText).
+int crc32_now(Call& c, uint32_t* out) {
+  Digest* d = c.d;
+  if (c.z) {
+    if (c.z->open) c.split();  // the leader's last Write is its own: settle, hashing it for the CRC only
+    else c.leave(true);
+  }
+  park(d);
+  if (d->latched) return d->latched;
+  *out = d->cbase.crc;
   return EFES_OK;
 }
 
@@ -286,6 +637,15 @@ int efes_pool_stats(efes_pool* p, uint32_t i, efes_queue_stats* out) {
   return efes_queue_get_stats(q, out);
 }
 
+int efes_pair_stats_get(efes_pair_stats* out) {
+  if (!out) return EFES_ERR_ARG;
+  out->pairs = g_pairs.load(std::memory_order_relaxed);
+  out->fused_writes = g_fused_writes.load(std::memory_order_relaxed);
+  out->fused_bytes = g_fused_bytes.load(std::memory_order_relaxed);
+  out->settles = g_settles.load(std::memory_order_relaxed);
+  return EFES_OK;
+}
+
 // ---- streaming SHA-1 (sha1digest) --------------------------------------------------------------
 int efes_sha1_new(efes_ctx* ctx, efes_sha1** out) { return sha1_alloc(ctx, nullptr, out, true); }
 int efes_sha1_new_zero(efes_ctx* ctx, efes_sha1** out) { return sha1_alloc(ctx, nullptr, out, false); }
@@ -298,9 +658,15 @@ void efes_sha1_free(efes_sha1* d) { digest_free(d); }
 
 void efes_sha1_reset(efes_sha1* d) {  // sha1.go:36-44: h = IV, nx = len = 0, x untouched
   if (!d) return;
-  std::lock_guard<std::mutex> lk(d->mu);
-  const efes_sha1_state cur = d->u ? efes::upload_shadow(d->u) : d->sbase;
-  drop(d);
+  Call c(d);
+  efes_sha1_state cur;
+  if (c.z) {
+    cur = efes::upload_shadow(c.z->u);  // x after the matched Writes: all of this digest's
+    c.leave(false);
+  } else {
+    cur = d->u ? efes::upload_shadow(d->u) : d->sbase;
+    drop(d);
+  }
   efes_sha1_state_init(&d->sbase);
   memcpy(d->sbase.x, cur.x, sizeof d->sbase.x);
   d->latched = EFES_OK;
@@ -313,10 +679,21 @@ int efes_sha1_write(efes_sha1* d, const void* p, size_t n) { return digest_write
 
 int efes_sha1_sum(efes_sha1* d, uint8_t out[20]) {  // sha1.go:82-87 (non-destructive)
   if (!d || !out) return EFES_ERR_ARG;
-  std::lock_guard<std::mutex> lk(d->mu);
-  int rc = acquire(d);
-  if (rc) return rc;
+  Call c(d);
   uint8_t s[24];
+  int rc;
+  if (c.z && !c.z->open) {
+    // the pair's Sum job (folded into the last chunk's fused job) computes both Sums; the
+    // follower takes its own and leaves the upload to the leader (whose Sum is its parked CRC)
+    rc = efes_upload_sum(c.z->u, s);
+    if (rc == EFES_OK) memcpy(out, s, 20);
+    else if (rc != EFES_ERR_STATE) d->latched = rc;  // checkSum's panic leaves the digest usable
+    c.leave(true);
+    return rc == EFES_OK && d->latched ? d->latched : rc;
+  }
+  if (c.z) c.split();
+  rc = acquire(d);
+  if (rc) return rc;
   rc = efes_upload_sum(d->u, s);
   if (rc == EFES_OK) memcpy(out, s, 20);
   else if (rc != EFES_ERR_STATE) d->latched = rc;  // checkSum's panic leaves the digest usable
@@ -326,9 +703,9 @@ int efes_sha1_sum(efes_sha1* d, uint8_t out[20]) {  // sha1.go:82-87 (non-destru
 
 int efes_sha1_marshal_text(efes_sha1* d, char out[200]) {  // sha1_efes.go:25-38
   if (!d || !out) return EFES_ERR_ARG;
-  std::lock_guard<std::mutex> lk(d->mu);
+  Call c(d);
   efes_sha1_state st;
-  const int rc = sha1_state_now(d, &st);
+  const int rc = sha1_state_now(c, &st);
   if (rc) return rc;
   efes_sha1_state_marshal_text(&st, out);
   return EFES_OK;
@@ -344,13 +721,14 @@ int efes_sha1_unmarshal_text(efes_sha1* d, const char* text, size_t n) {  // sha
 
 int efes_sha1_get_state(efes_sha1* d, efes_sha1_state* out) {
   if (!d || !out) return EFES_ERR_ARG;
-  std::lock_guard<std::mutex> lk(d->mu);
-  return sha1_state_now(d, out);
+  Call c(d);
+  return sha1_state_now(c, out);
 }
 
 int efes_sha1_set_state(efes_sha1* d, const efes_sha1_state* in) {
   if (!d || !in) return EFES_ERR_ARG;
-  std::lock_guard<std::mutex> lk(d->mu);
+  Call c(d);
+  if (c.z) c.leave(false);
   drop(d);
   d->sbase = *in;
   d->latched = EFES_OK;
@@ -365,7 +743,8 @@ void efes_crc32_free(efes_crc32* d) { digest_free(d); }
 
 void efes_crc32_reset(efes_crc32* d) {  // crc32.go:74
   if (!d) return;
-  std::lock_guard<std::mutex> lk(d->mu);
+  Call c(d);
+  if (c.z) c.leave(false);
   drop(d);
   d->cbase.crc = 0;
   d->latched = EFES_OK;
@@ -378,11 +757,8 @@ int efes_crc32_write(efes_crc32* d, const void* p, size_t n) { return digest_wri
 
 int efes_crc32_sum32(efes_crc32* d, uint32_t* out) {  // crc32.go:88
   if (!d || !out) return EFES_ERR_ARG;
-  std::lock_guard<std::mutex> lk(d->mu);
-  park(d);
-  if (d->latched) return d->latched;
-  *out = d->cbase.crc;
-  return EFES_OK;
+  Call c(d);
+  return crc32_now(c, out);
 }
 
 int efes_crc32_sum(efes_crc32* d, uint8_t out[4]) {  // crc32.go:90-93
@@ -407,7 +783,8 @@ int efes_crc32_unmarshal_text(efes_crc32* d, const char* text, size_t n) {  // c
   efes_crc32_state s;
   const int rc = efes_crc32_state_unmarshal_text(&s, text, n);
   if (rc) return rc;
-  std::lock_guard<std::mutex> lk(d->mu);
+  Call c(d);
+  if (c.z) c.leave(false);
   drop(d);
   d->cbase = s;
   d->latched = EFES_OK;

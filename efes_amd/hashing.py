@@ -23,7 +23,7 @@ import threading
 
 import numpy as np
 
-from ._lib import MODE_AUTO, EfesError, Plan, QueueStats, Sha1State, check, lib
+from ._lib import MODE_AUTO, EfesError, PairStats, Plan, QueueStats, Sha1State, check, lib
 
 __all__ = ["Context", "default_context", "crc32_combine", "Sha1Digest", "CRC32Digest", "Sha1File", "Digest", "FileInfo",
            "new_sha1", "new_crc32_ieee", "EfesError"]
@@ -79,6 +79,10 @@ class Context:
         at crc_state_ptr, segment-parallel over the whole GPU (asynchronous on `stream`)."""
         check(lib().efes_crc32_span(self.handle, data_ptr, nbytes, crc_state_ptr, stream), "efes_crc32_span")
 
+    def debug_fault_after(self, k: int) -> None:
+        """Test hook (efes_debug_fault_after): the k-th launch of this context's digest queue faults."""
+        check(lib().efes_debug_fault_after(self.handle, k), "efes_debug_fault_after")
+
     def copy_to_host(self, dst_host: int, src_device: int, nbytes: int, stream: int | None = None) -> None:
         check(lib().efes_copy_to_host(self.handle, dst_host, src_device, nbytes, stream), "efes_copy_to_host")
 
@@ -119,6 +123,27 @@ class Pool:
         h = ctypes.c_void_p()
         check(lib().efes_pool_create(arr, len(self.ctxs), ctypes.byref(h)), "efes_pool_create")
         self.handle = h
+        self._mu = threading.Lock()
+        self._live = 0  # digests made on the pool and not yet freed
+        self._closing = False
+
+    def _adopt(self) -> None:  # a digest is being made on the pool
+        with self._mu:
+            if self._closing or not self.handle:
+                raise EfesError(-4, "pool closed")
+            self._live += 1
+
+    def _release(self) -> None:  # a digest of the pool was freed
+        with self._mu:
+            self._live -= 1
+            last = self._closing and self._live == 0
+        if last:
+            self._destroy()
+
+    def _destroy(self) -> None:
+        if self.handle:
+            lib().efes_pool_destroy(self.handle)
+            self.handle = None
 
     def stats(self, i: int) -> QueueStats:
         """Counters of the digest queue of context i (efes_pool_stats)."""
@@ -126,10 +151,21 @@ class Pool:
         check(lib().efes_pool_stats(self.handle, i, ctypes.byref(st)), "efes_pool_stats")
         return st
 
-    def close(self) -> None:  # after every digest of the pool is freed
-        if self.handle:
-            lib().efes_pool_destroy(self.handle)
-            self.handle = None
+    def close(self) -> None:
+        """efes_pool_destroy -- deferred until the last digest made on the pool is freed (the C pool
+        must outlive its digests: a Write of a live digest re-reads the pool's contexts)."""
+        with self._mu:
+            self._closing = True
+            now = self._live == 0
+        if now:
+            self._destroy()
+
+
+def pair_stats() -> dict:
+    """efes_pair_stats_get (ABI 6): process-wide counters of fused CRC + SHA-1 digest pairs."""
+    st = PairStats()
+    check(lib().efes_pair_stats_get(ctypes.byref(st)), "efes_pair_stats_get")
+    return {f: int(getattr(st, f)) for f, _ in PairStats._fields_}
 
 
 def crc32_combine(crc1: int, crc2: int, len2: int) -> int:
@@ -148,10 +184,15 @@ class Sha1Digest:
 
     def __init__(self, ctx: Context | None = None, reset: bool = True, pool: Pool | None = None):
         h = ctypes.c_void_p()
-        if pool is not None:  # the pool must outlive its digests: keep a reference
-            self.ctx, self.pool = None, pool
+        if pool is not None:  # the pool must outlive its digests: keep a reference, count this one
+            self.ctx, self.pool = None, None
+            pool._adopt()
             fn = lib().efes_sha1_new_pool if reset else lib().efes_sha1_new_zero_pool
-            check(fn(pool.handle, ctypes.byref(h)), "efes_sha1_new_pool")
+            rc = fn(pool.handle, ctypes.byref(h))
+            if rc:
+                pool._release()
+            check(rc, "efes_sha1_new_pool")
+            self.pool = pool
         else:
             self.ctx, self.pool = ctx or default_context(), None
             fn = lib().efes_sha1_new if reset else lib().efes_sha1_new_zero
@@ -162,6 +203,8 @@ class Sha1Digest:
         if getattr(self, "_h", None):
             lib().efes_sha1_free(self._h)
             self._h = None
+            if getattr(self, "pool", None) is not None:
+                self.pool._release()
 
     def reset(self) -> None:  # sha1.go:36-44
         lib().efes_sha1_reset(self._h)
@@ -209,8 +252,13 @@ class CRC32Digest:
     def __init__(self, ctx: Context | None = None, pool: Pool | None = None):
         h = ctypes.c_void_p()
         if pool is not None:
-            self.ctx, self.pool = None, pool
-            check(lib().efes_crc32_new_pool(pool.handle, ctypes.byref(h)), "efes_crc32_new_pool")
+            self.ctx, self.pool = None, None
+            pool._adopt()
+            rc = lib().efes_crc32_new_pool(pool.handle, ctypes.byref(h))
+            if rc:
+                pool._release()
+            check(rc, "efes_crc32_new_pool")
+            self.pool = pool
         else:
             self.ctx, self.pool = ctx or default_context(), None
             check(lib().efes_crc32_new(self.ctx.handle, ctypes.byref(h)), "efes_crc32_new")
@@ -220,6 +268,8 @@ class CRC32Digest:
         if getattr(self, "_h", None):
             lib().efes_crc32_free(self._h)
             self._h = None
+            if getattr(self, "pool", None) is not None:
+                self.pool._release()
 
     def reset(self) -> None:  # crc32.go:74
         lib().efes_crc32_reset(self._h)

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define EFES_ABI_VERSION 5
+#define EFES_ABI_VERSION 6
 
 /* ---- error codes ---------------------------------------------------------------- */
 #define EFES_OK 0
@@ -280,6 +280,28 @@ int efes_queue_get_stats(efes_queue* q, efes_queue_stats* out);
 typedef struct efes_sha1 efes_sha1;
 typedef struct efes_crc32 efes_crc32;
 
+/* Fused pairs (ABI 6).  io.MultiWriter(f, CRC32, Sha1) (filereceiver.go:208-209) hands every body
+ * buffer to the CRC digest and then, unchanged, to the SHA-1 digest.  The library detects that
+ * pattern and binds the two digests to ONE upload keeping both hashes, so each byte is staged once
+ * and hashed by one fused job, as efes_upload_* does for a caller that asks for it:
+ *   - a CRC digest's Write that opens a fresh upload is a candidate; a parked SHA-1 digest's Write
+ *     with the same pointer and length binds to it when the staged bytes equal its own (memcmp);
+ *   - then each CRC Write is staged but held back until the SHA-1 Write of the same (p, n), checked
+ *     against the staged bytes, confirms it;
+ *   - anything else (a Write to one digest only, other bytes, the CRC digest synced first, Reset /
+ *     UnmarshalText / free of one, an eviction) splits the pair: every confirmed byte is in both
+ *     states, an unconfirmed CRC Write in the CRC state only, and both go on alone.
+ * Every digest therefore hashes exactly the bytes of its own Writes, in order, whatever the caller
+ * does; only the speed depends on the pattern.  EFES_DIGEST_FUSE=0 (env) disables binding.
+ * Process-wide counters: */
+typedef struct efes_pair_stats {
+    uint64_t pairs;         /* CRC + SHA-1 digests bound to one upload */
+    uint64_t fused_writes;  /* SHA-1 Writes served by the CRC Write's staged bytes (no copy, no job) */
+    uint64_t fused_bytes;   /* their bytes */
+    uint64_t settles;       /* pairs split (diverging Writes, evictions) */
+} efes_pair_stats;
+int efes_pair_stats_get(efes_pair_stats* out);
+
 int efes_sha1_new(efes_ctx* ctx, efes_sha1** out);                       /* sha1.go:48-52 NewSha1 */
 int efes_sha1_new_zero(efes_ctx* ctx, efes_sha1** out);                  /* `var d sha1digest` (zero value) */
 void efes_sha1_free(efes_sha1* d);
@@ -342,6 +364,11 @@ uint32_t efes_crc32_combine(uint32_t crc1, uint32_t crc2, uint64_t len2);
  * context stream); calls that share a state must be ordered on one stream. */
 int efes_crc32_span(efes_ctx* ctx, const void* data_device, uint64_t length, efes_crc32_state* crc_device,
                     void* stream);
+
+/* Test hook (ABI 6): the k-th launch from now of ctx's digest queue (k = 0: none) reports a device
+ * fault instead of running, as a faulted kernel would, and the queue stays faulted.  For the
+ * fault-latching tests of the Go surface; an explicit call, so no environment can switch it on. */
+int efes_debug_fault_after(efes_ctx* ctx, uint64_t k);
 
 /* Pure text codecs on plain states (no device work). */
 void efes_sha1_state_marshal_text(const efes_sha1_state* s, char out[200]);

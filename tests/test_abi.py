@@ -215,3 +215,41 @@ def test_integration_doc_covers_every_declared_symbol():
     doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
     missing = [n for n in declared_functions() if not re.search(r"\b%s\b" % n, doc)]
     assert not missing, missing
+
+
+def test_pool_close_waits_for_its_digests(efes_lib):
+    """Pool.close() while digests made on the pool are alive must not free the C pool
+    under them (their next Write re-reads its contexts).  The destroy is deferred to the last
+    digest's free.  Host-only: a pooled digest touches no device until its first Write, so stand-in
+    context handles suffice."""
+    from efes_amd import hashing
+
+    class FakeCtx:
+        handle = ctypes.c_void_p(0x1000)
+
+    pool = hashing.Pool([FakeCtx()])
+    s, c = hashing.Sha1Digest(pool=pool), hashing.CRC32Digest(pool=pool)
+    pool.close()
+    assert pool.handle  # two digests still alive
+    del s
+    assert pool.handle
+    del c
+    assert pool.handle is None  # the last one freed it
+    with pytest.raises(hashing.EfesError):
+        hashing.Sha1Digest(pool=pool)
+
+
+def test_pair_stats_layout(tmp_path, efes_lib):
+    """efes_pair_stats (ABI 6) as the C compiler lays it out = the ctypes mirror; counters readable
+    without a GPU."""
+    src = tmp_path / "p.c"
+    src.write_text('#include <stddef.h>\n#include <stdio.h>\n#include "efes_hash.h"\nint main(void){printf("%zu %zu %zu\\n",'
+                   ' sizeof(efes_pair_stats), offsetof(efes_pair_stats, fused_bytes), offsetof(efes_pair_stats, settles));'
+                   'return 0;}\n')
+    exe = tmp_path / "p"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()
+    P = efes_lib.PairStats
+    assert [int(x) for x in out] == [ctypes.sizeof(P), P.fused_bytes.offset, P.settles.offset]
+    st = P()
+    assert efes_lib.lib().efes_pair_stats_get(ctypes.byref(st)) == 0

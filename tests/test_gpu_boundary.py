@@ -41,6 +41,16 @@ def small_ctx(gpu, monkeypatch):
     ctx.close()
 
 
+class _Counts(dict):
+    def __sub__(self, o):
+        return _Counts({k: self[k] - o[k] for k in self})
+
+
+def pair_stats(gpu) -> _Counts:
+    """efes_pair_stats_get (ABI 6): process-wide fused-pair counters."""
+    return _Counts(gpu["hashing"].pair_stats())
+
+
 def _payload(n: int, seed: int) -> bytes:
     return random.Random(seed).randbytes(n)
 
@@ -79,6 +89,7 @@ def test_200_patches_new_fileinfo_each_never_freed(gpu, small_ctx, oracle):
     is freed before the end.  Every Write succeeds; every .info text and Sum equals the oracle's."""
     hashing = gpu["hashing"]
     pool1 = hashing.Pool([small_ctx])  # only to read the digest queue's counters
+    p0 = pair_stats(gpu)
     objs = 20
     bodies = {o: [_payload(random.Random(o * 100 + p).choice([1, 63, 64, 65, 4097, 40000, 65536, 70001, 131072]),
                            o * 1000 + p) for p in range(10)] for o in range(objs)}
@@ -106,7 +117,12 @@ def test_200_patches_new_fileinfo_each_never_freed(gpu, small_ctx, oracle):
                 assert fi.digest.sha1.marshal_text().decode() == expect[o].sha.marshal_text()
     st = pool1.stats(0)
     assert st.max_uploads == 15 and st.free_uploads == 15  # every digest is parked after its sync point
-    assert st.jobs > 0 and st.bytes == sum(len(b) for bs in bodies.values() for b in bs) * 2
+    # every PATCH's MultiWriter pair was fused: each body byte staged and hashed ONCE (two separate
+    # digests hashed it twice until round 3)
+    total = sum(len(b) for bs in bodies.values() for b in bs)
+    assert st.jobs > 0 and st.bytes == total, (st.bytes, total)
+    ps = pair_stats(gpu) - p0
+    assert ps["pairs"] == 200 and ps["fused_bytes"] == total and ps["settles"] == 0, ps
     del alive
     pool1.close()
 
@@ -168,20 +184,19 @@ def test_concurrent_threads_more_digests_than_slots(gpu, small_ctx, oracle):
     assert not errors, errors[:3]
 
 
-def test_device_fault_is_latched_to_the_sync_point(gpu, monkeypatch, oracle):
-    """A device fault under the Writes (EFES_FAULT_INJECT_LAUNCH=1: the queue's first launch reports
-    a fault, as a faulted kernel would): every Write keeps returning len(p) -- Go's Write never
-    fails -- and MarshalText / Sum report the fault (MarshalText's error -> HTTP 500).  The queue
-    stays faulted, as after a real device fault (a new digest there also fails at its sync point),
-    while a digest on a healthy context is unaffected."""
+def test_device_fault_is_latched_to_the_sync_point(gpu, oracle):
+    """A device fault under the Writes (efes_debug_fault_after(ctx, 1): the digest queue's first
+    launch reports a fault, as a faulted kernel would): every Write keeps returning len(p) -- Go's
+    Write never fails -- and MarshalText / Sum report the fault (MarshalText's error -> HTTP 500).
+    The queue stays faulted, as after a real device fault (a new digest there also fails at its sync
+    point), while a digest on a healthy context is unaffected."""
     hashing, efes = gpu["hashing"], gpu["efes"]
-    monkeypatch.setenv("EFES_FAULT_INJECT_LAUNCH", "1")
     ctx = hashing.Context(0)
+    ctx.debug_fault_after(1)
     d = d2 = None
     try:
         d = hashing.Digest(ctx)
-        assert d.write(b"x") == 1  # creates the context's digest queue while the hook is set
-        monkeypatch.delenv("EFES_FAULT_INJECT_LAUNCH")
+        assert d.write(b"x") == 1
         for k in range(8):
             assert d.write(_payload(65536 + k, 10 + k)) == 65536 + k
         with pytest.raises(efes.EfesError) as e:
@@ -258,3 +273,34 @@ def test_pool_spreads_digests_over_contexts(gpu, oracle):
     pool.close()
     for c in ctxs:
         c.close()
+
+
+def test_pool_skips_a_faulted_context(gpu, oracle):
+    """a pooled digest opens its upload on the context with the most free slots -- but
+    never on one whose digest queue latched a device fault (its uploads close fast and would look
+    free).  Context 0's queue faults on its first launch; afterwards every new pooled digest lands
+    on context 1 and equals the oracle, and context 0's queue launches nothing more."""
+    hashing, efes = gpu["hashing"], gpu["efes"]
+    ctxs = [hashing.Context(0), hashing.Context(0)]
+    ctxs[0].debug_fault_after(1)
+    pool = hashing.Pool(ctxs)
+    try:
+        # fault context 0: open digests until one lands there, then sync it
+        d = hashing.Digest(ctx=ctxs[0])
+        d.write(b"fault me")
+        with pytest.raises(efes.EfesError):
+            d.sha1.marshal_text()
+        del d
+        s0 = pool.stats(0)
+        for i in range(24):
+            body = _payload(70000 + i, 500 + i)
+            fi = hashing.FileInfo(pool=pool)
+            _patch(hashing, fi, body)
+            assert fi.digest.sha1.marshal_text().decode() == _oracle_text(oracle, body), i
+            assert fi.digest.crc32.sum32() == zlib.crc32(body), i
+        assert pool.stats(0).launches == s0.launches  # nothing more went to the faulted queue
+        assert pool.stats(1).jobs > 0
+    finally:
+        pool.close()
+        for c in ctxs:
+            c.close()

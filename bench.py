@@ -93,6 +93,10 @@ def parse_args(argv=None):
     p.add_argument("--uploads-leg", choices=["auto", "on", "off"], default="auto",
                    help="also report the server path (tools/bench_uploads: 32 request threads x 256 uploads in "
                         "flight, 8192 x 4 MiB, 32 KiB pageable Writes, Sum each); auto = N=1 only")
+    p.add_argument("--go-surface-leg", choices=["auto", "on", "off"], default="auto",
+                   help="also report the UNCHANGED Go surface (tools/bench_go_surface: hash_gpu.go's calls under "
+                        "saveFile, fused MultiWriter pairs and EFES_DIGEST_FUSE=0) at uploads_path's concurrency "
+                        "(auto: N=1)")
     p.add_argument("--receiver-leg", choices=["auto", "on", "off"], default="auto",
                    help="also report the receiver with files (tools/bench_receiver: saveFile through ServeHTTP, "
                         "768 request threads x 4 MiB PATCHes on tmpfs) and Sha1File read-back (256 threads); auto = N=1 only")
@@ -246,6 +250,42 @@ def uploads_workload(args, ctx):
     want = hashlib.sha1(src).hexdigest() + "%08x" % zlib.crc32(src)
     res["digests_match"] = res.pop("sum_sha1_crc32") == want and res.pop("all_sums_equal")
     res["note"] = "native request threads: pageable Writes -> pinned staging -> batched launches -> per-upload Sum"
+    return res
+
+
+def go_surface_leg(uploads=None):
+    """The drop-in boundary as unchanged Go code calls it (efes_hash.h layer 2; INTEGRATION.md §2's
+    hash_gpu.go under filereceiver.go's saveFile), driven natively by tools/bench_go_surface at
+    uploads_path's concurrency (32 request threads x 256 uploads in flight, 8 192 x 4 MiB, 32 KiB
+    io.Copy buffers): per PATCH efes_sha1_new_pool + efes_crc32_new_pool, efes_crc32_write then
+    efes_sha1_write of the SAME buffer (MultiWriter(f, CRC32, Sha1), filereceiver.go:208-209), Sum of
+    both.  The library fuses each pair into one upload (efes_stream.cpp); the same run with
+    EFES_DIGEST_FUSE=0 (two uploads, each byte staged and hashed twice) is reported beside it.
+    Digests checked against hashlib/zlib.  Returns the result dict (not the metric)."""
+    import hashlib
+    import subprocess
+    import zlib
+
+    exe = os.path.join(ROOT, "tools", "bench_go_surface")
+    cmd = [exe, "32", "8192", str(4 << 20), str(32 << 10), "256", "1", "256", "8208"]
+
+    def run(fuse):
+        r = subprocess.run(cmd, check=True, capture_output=True, text=True, timeout=300,
+                           env=dict(os.environ, EFES_DIGEST_FUSE=fuse))
+        return json.loads(r.stdout.strip().splitlines()[-1])
+
+    src = _xorshift_bytes(4 << 20)
+    want = hashlib.sha1(src).hexdigest() + "%08x" % zlib.crc32(src)
+    res = run("1")
+    res["digests_match"] = res.pop("sum_sha1_crc32") == want and res.pop("all_equal")
+    un = run("0")
+    res["unfused"] = {"value": un["value"], "unit": "GiB/s", "hashed_bytes_per_byte": un["hashed_bytes_per_byte"],
+                      "launches": un["launches"], "digests_match": un["sum_sha1_crc32"] == want and un["all_equal"],
+                      "note": "EFES_DIGEST_FUSE=0: the CRC and SHA-1 digests as two uploads"}
+    if uploads and uploads.get("value"):
+        res["vs_uploads_path"] = round(res["value"] / uploads["value"], 4)
+    res["note"] = ("unchanged Go call sequence (hash_gpu.go): pooled NewSha1 + NewCRC32IEEE per PATCH, 32 KiB "
+                   "CRC-then-SHA-1 Writes of one buffer, Sum; the pair fused into one upload by the library")
     return res
 
 
@@ -842,6 +882,8 @@ def main(argv=None):
             a = argparse.Namespace(**vars(args))
             a.upload_threads, a.uploads, a.open_per_thread, a.upload_bytes = 32, 8192, 256, 4 << 20
             out["uploads_path"] = uploads_workload(a, ctx)
+        if args.go_surface_leg == "on" or (args.go_surface_leg == "auto" and world == 1):
+            out["go_surface_path"] = go_surface_leg(out.get("uploads_path"))
         if args.receiver_leg == "on" or (args.receiver_leg == "auto" and world == 1):
             out["receiver_path"] = receiver_leg()
         if args.drain_leg == "on" or (args.drain_leg == "auto" and world == 1):

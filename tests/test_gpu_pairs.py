@@ -55,10 +55,12 @@ class Obj:
         self.oracle = oracle
 
     def crc_write(self, buf, off, n):
+        assert off + n <= len(buf)
         self.g["check"](self.g["lib"].efes_crc32_write(self.crc._h, ctypes.addressof(buf) + off, n), "crc write")
         self.ocrc.write(bytes(buf[off:off + n]))
 
     def sha_write(self, buf, off, n):
+        assert off + n <= len(buf)
         self.g["check"](self.g["lib"].efes_sha1_write(self.sha._h, ctypes.addressof(buf) + off, n), "sha write")
         assert self.osha.write(bytes(buf[off:off + n])) == 0
 
@@ -94,11 +96,12 @@ OPS = ["mw", "mw", "mw", "mw", "crc_only", "sha_only", "mutated", "other_len", "
 def _script(gpu, oracle, rng: random.Random, steps: int, ctx=None, pool=None, tag=""):
     """A random sequence of Go-surface calls on one object; every sync point compared with the oracle."""
     o = Obj(gpu, oracle, ctx, pool)
-    buf = _buf(300_000, rng.randrange(1 << 30))
+    size = 400_000  # every Write stays inside: off < 230 000, n <= 165 536
+    buf = _buf(size, rng.randrange(1 << 30))
     for k in range(steps):
         op = rng.choice(OPS)
         n = rng.choice([1, 55, 64, 4096, 32768, 32768, 40000, 65536])
-        off = rng.randrange(0, 300_000 - 140_000)
+        off = rng.randrange(0, size - 170_000)
         t = f"{tag} step {k} {op} n={n}"
         if op == "mw":  # the MultiWriter pattern: CRC then SHA-1, same (p, n)
             o.crc_write(buf, off, n)

@@ -1225,3 +1225,38 @@ def test_full_size_ingest_launch_wide_equals_group4(env):
         assert wide_sha[i] == wide_sha[i + slots] and wide_crc[i] == wide_crc[i + slots]
     assert len(set(wide_sha)) == slots
     _spot_check(env, buf, offs, lengths, wide_sha, wide_crc, [0, 1, 65535, m - 1])
+
+
+def test_full_size_ingest_segmented_as_benched(env):
+    """BASELINE configs[4] exactly as bench.py's ingest leg runs it since round 3 (bench.py ingest
+    workload, --ingest-segment 1 MiB): 196 608 chunks of 4 MiB, each arriving as four 1 MiB segment
+    Writes from a 192 GiB buffer of distinct bytes (chunk j = its 1 MiB segment, four times), the
+    states resident in HBM between the four launches -- the first EFES_JOB_INIT, the last
+    EFES_JOB_FINALIZE: the per-PATCH resume of filereceiver.go:182-226 at full occupancy -- in WIDE
+    (AUTO's shape at this count, paced at three waves per SIMD), against GROUP4 running the same
+    four segments on states of its own: every digest and CRC agrees, and 8 chunks (the first and
+    the last job among them) match hashlib/zlib of the 4 MiB they stand for."""
+    from efes_amd._lib import MODE_GROUP
+    torch = env["torch"]
+    seg, m, nseg = 1 << 20, 196608, 4
+    buf = torch.empty(m * seg, dtype=torch.uint8, device="cuda:0")
+    env["ctx"].fill_synthetic(buf.data_ptr(), buf.numel(), 0x1A6E57, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    offs, lengths = np.arange(m, dtype=np.uint64) * np.uint64(seg), np.full(m, seg, np.uint64)
+    assert env["hashing"].lib().efes_auto_mode(env["ctx"].handle, m) == env["efes"].MODE_WIDE
+    got = {}
+    for mode in (env["efes"].MODE_WIDE, MODE_GROUP[4]):
+        base = env["DeviceBatch"](buf.data_ptr(), offs, lengths, fresh=False, ctx=env["ctx"])
+        for k in range(nseg):
+            base.variant(fresh=k == 0, finalize=k == nseg - 1).run(mode)
+        assert (base.status_host() == 0).all(), mode
+        got[mode] = (base.sha1_hex(), base.crc_sum().copy())
+        del base
+    (ws, wc), (gs, gc) = got[env["efes"].MODE_WIDE], got[MODE_GROUP[4]]
+    assert ws == gs and (wc == gc).all()
+    assert len(set(ws)) == m  # distinct bytes, distinct digests
+    for j in (0, 1, 4095, 65535, 65536, 131071, 131072, m - 1):
+        chunk = buf[j * seg:(j + 1) * seg].cpu().numpy().tobytes() * nseg
+        assert ws[j] == hashlib.sha1(chunk).hexdigest() and int(wc[j]) == zlib.crc32(chunk), j
+    del buf
+    torch.cuda.empty_cache()

@@ -14,3 +14,5 @@ for i in 1 2; do
 done
 timeout -k 10 120 tools/bench_go_surface 32 8192 4194304 32768 256 4 256 8208 > "$out/go_fused_4patches.json"
 cat "$out"/*.json
+timeout -k 10 300 python -u -m pytest -x -v --timeout 200 --timeout-method thread \
+  "tests/test_gpu_parity.py::test_full_size_ingest_segmented_as_benched" > "$out/test_cfg4_segmented.log" 2>&1

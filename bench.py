@@ -97,6 +97,8 @@ def parse_args(argv=None):
                    help="also report the UNCHANGED Go surface (tools/bench_go_surface: hash_gpu.go's calls under "
                         "saveFile, fused MultiWriter pairs and EFES_DIGEST_FUSE=0) at uploads_path's concurrency "
                         "(auto: N=1)")
+    p.add_argument("--latency-leg", choices=["auto", "on", "off"], default="auto",
+                   help="also report per-PATCH latency at 1/16/256 uploads in flight, GPU vs the CPU port (auto: N=1)")
     p.add_argument("--receiver-leg", choices=["auto", "on", "off"], default="auto",
                    help="also report the receiver with files (tools/bench_receiver: saveFile through ServeHTTP, "
                         "768 request threads x 4 MiB PATCHes on tmpfs) and Sha1File read-back (256 threads); auto = N=1 only")
@@ -287,6 +289,37 @@ def go_surface_leg(uploads=None):
     res["note"] = ("unchanged Go call sequence (hash_gpu.go): pooled NewSha1 + NewCRC32IEEE per PATCH, 32 KiB "
                    "CRC-then-SHA-1 Writes of one buffer, Sum; the pair fused into one upload by the library")
     return res
+
+
+def patch_latency_leg():
+    """Per-PATCH latency of one 4 MiB PATCH (saveFile's hashing: MultiWriter CRC-then-SHA-1 Writes in
+    32 KiB buffers, then both Sums) with 1, 16 and 256 uploads in flight: the unchanged Go surface on
+    the GPU (tools/bench_go_surface, one PATCH per request thread, fused pairs) against the CPU port
+    of the same hashing on the box's CPU quota (oracle/patch_cpu, the reference's algorithm; a
+    reported baseline).  Both hash the same bytes; digests checked against hashlib/zlib."""
+    import hashlib
+    import subprocess
+    import zlib
+
+    src = _xorshift_bytes(4 << 20)
+    want = hashlib.sha1(src).hexdigest() + "%08x" % zlib.crc32(src)
+
+    def run(argv):
+        r = subprocess.run(argv, check=True, capture_output=True, text=True, timeout=300)
+        return json.loads(r.stdout.strip().splitlines()[-1])
+
+    points = []
+    for k, rounds in ((1, 20), (16, 8), (256, 4)):
+        g = run([os.path.join(ROOT, "tools", "bench_go_surface"), str(k), str(k * rounds), str(4 << 20), str(32 << 10),
+                 "1", "1", "256", "1024"])
+        c = run([os.path.join(ROOT, "oracle", "patch_cpu"), str(k), str(4 << 20), "3"])
+        points.append({"uploads_in_flight": k, "gpu_patch_ms": g["patch_group_ms"], "gpu_GiB/s": g["value"],
+                       "cpu_patch_ms": c["patch_ms"], "cpu_GiB/s": c["value"], "cpu_threads_pinned": c["pinned_cpus"],
+                       "digests_match": g["sum_sha1_crc32"] == want and g["all_equal"] and
+                       c["sum_sha1_crc32"] == want and c["all_equal"]})
+    return {"patch_bytes": 4 << 20, "points": points,
+            "note": "GPU: unchanged Go surface, one PATCH per request thread; CPU: oracle port of the same hashing "
+                    "(kind port) on the quota's cores; latency = one PATCH's Writes + Sums; not `value`"}
 
 
 def receiver_leg():
@@ -884,6 +917,8 @@ def main(argv=None):
             out["uploads_path"] = uploads_workload(a, ctx)
         if args.go_surface_leg == "on" or (args.go_surface_leg == "auto" and world == 1):
             out["go_surface_path"] = go_surface_leg(out.get("uploads_path"))
+        if args.latency_leg == "on" or (args.latency_leg == "auto" and world == 1):
+            out["patch_latency"] = patch_latency_leg()
         if args.receiver_leg == "on" or (args.receiver_leg == "auto" and world == 1):
             out["receiver_path"] = receiver_leg()
         if args.drain_leg == "on" or (args.drain_leg == "auto" and world == 1):

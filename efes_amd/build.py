@@ -48,6 +48,18 @@ def build_lib(force: bool = False, verbose: bool = False) -> str:
     return LIB
 
 
+def build_variant(name: str, defines: list[str]) -> str:
+    """An A/B build of the library with extra -D flags: efes_amd/lib/libefeshash_<name>.so (loaded through
+    EFES_LIB_OVERRIDE by the tools/gpu_*_ab.sh scripts; never the product)."""
+    out = os.path.join(LIB_DIR, f"libefeshash_{name}.so")
+    srcs = [os.path.join(CSRC, s) for s in SOURCES]
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", *[f"-D{d}" for d in defines],
+           "-I", os.path.join(ROOT, "include"), "-o", out + ".tmp"] + srcs
+    subprocess.run(cmd, check=True)
+    os.replace(out + ".tmp", out)
+    return out
+
+
 def build_tools() -> list[str]:
     """Native benchmark drivers under tools/ (link the in-tree library; not part of the product)."""
     out = []
@@ -127,6 +139,9 @@ def build_oracle() -> str:
 
 
 if __name__ == "__main__":
+    if len(sys.argv) > 2 and sys.argv[1] == "--variant":  # python -m efes_amd.build --variant NAME DEFINE...
+        print(build_variant(sys.argv[2], sys.argv[3:]))
+        sys.exit(0)
     print(build_lib(force="--force" in sys.argv, verbose=True))
     print(build_tools())
     print(build_oracle())

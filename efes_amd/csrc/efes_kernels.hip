@@ -1367,6 +1367,26 @@ __device__ __forceinline__ void wide_bulk(const uint8_t* q, uint64_t nbulk, uint
   load_block_le<kAligned16>(src(0), A);
   load_block_le<kAligned16>(src(1), B);
   uint64_t b = 0;
+#ifndef EFES_WIDE_BLOCKLOADS
+  // Uniform phase (blocks b..b+5 exist in every lane), a 128-B line at a time: the two blocks of a
+  // line are loaded back to back (eight dwordx4), one block-time before the first is hashed.  A
+  // lane's blocks loaded one at a time, a block apart (the A/B build below), fetched 14.5 % more
+  // than the message from HBM (FETCH_SIZE x 2, calibrated on this access pattern with
+  // tools/microbench/mb_wide_fetch: profiles/r04_fetch/): the second half of a line was often
+  // evicted from L2 before the lane came back for it.  A holds the even block, B / C the odd one.
+  for (; b + 5 < nmin; b += 4) {
+    if (b % 8 == 0) wide_pace(prog, w, nw, (uint32_t)b);  // every 8 blocks
+    const uint8_t* qb = q + 64 * b;
+    wide_step<kSha, kCrc>(A, t, h, crc_raw, true);
+    load_block_le<kAligned16>(qb + 128, A);
+    load_block_le<kAligned16>(qb + 192, C);
+    wide_step<kSha, kCrc>(B, t, h, crc_raw, true);
+    wide_step<kSha, kCrc>(A, t, h, crc_raw, true);
+    load_block_le<kAligned16>(qb + 256, A);
+    load_block_le<kAligned16>(qb + 320, B);
+    wide_step<kSha, kCrc>(C, t, h, crc_raw, true);
+  }
+#else
   for (; b + 4 < nmin; b += 3) {  // uniform phase: blocks b..b+4 exist in every lane
     if (b % 6 == 0) wide_pace(prog, w, nw, (uint32_t)b);  // every 6 blocks: ~4 VALU per block
     const uint8_t* qb = q + 64 * b;
@@ -1377,6 +1397,7 @@ __device__ __forceinline__ void wide_bulk(const uint8_t* q, uint64_t nbulk, uint
     load_block_le<kAligned16>(qb + 256, B);
     wide_step<kSha, kCrc>(C, t, h, crc_raw, true);
   }
+#endif
   for (; b < nmax; b += 3) {  // ragged phase (A, B hold blocks b, b+1 or the dummy)
     if (b % 6 == 0) wide_pace(prog, w, nw, (uint32_t)b);
     load_block_le<kAligned16>(src(b + 2), C);

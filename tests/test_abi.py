@@ -253,3 +253,29 @@ def test_pair_stats_layout(tmp_path, efes_lib):
     assert [int(x) for x in out] == [ctypes.sizeof(P), P.fused_bytes.offset, P.settles.offset]
     st = P()
     assert efes_lib.lib().efes_pair_stats_get(ctypes.byref(st)) == 0
+
+
+def test_integration_doc_two_build_targets():
+    """the -tags efesgpu build swaps the digests for the whole binary, so the
+    integration names two targets -- the storage server with the GPU digests, the single-stream CLI
+    (efes write / efes drain) on the reference's unchanged pure-Go build -- with the Makefile and
+    goreleaser lines, and no run-time routing between the paths."""
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    sec = doc[doc.index("## 1. Build"):doc.index("## 2.")]
+    # the server target: tagged cgo build, its own binary and archive carrying the library
+    assert "CGO_ENABLED=1 go build -tags efesgpu -o $(NAME)-server" in sec
+    assert "binary: efes-server" in sec and "flags: [-tags=efesgpu]" in sec
+    assert "efes_amd/lib/libefeshash.so" in sec
+    # the CLI target: the reference's own lines, unchanged
+    assert "GOOS=linux GOARCH=amd64 CGO_ENABLED=0 go build -o $(NAME)" in sec
+    assert "`Makefile:6`" in sec and "`.goreleaser.yml:9`" in sec
+    for role in ("`write`", "`drain`", "`server`"):
+        assert role in sec, role
+    # the reason, measured: one stream on the GPU vs one core
+    assert "0.084 GiB/s" in sec and "0.60 GiB/s" in sec
+    assert "No binary routes between the two" in sec
+    # the reference lines cited are the ones that build with CGO_ENABLED=0
+    ref = "/root/reference"
+    if os.path.isdir(ref):
+        assert "CGO_ENABLED=0 go build" in open(os.path.join(ref, "Makefile")).read().split("\n")[5]
+        assert "CGO_ENABLED=0" in open(os.path.join(ref, ".goreleaser.yml")).read().split("\n")[8]

@@ -541,10 +541,13 @@ def make_workload(args, rank: int, world: int, ctx, device: str, stream):
 # Instruction-issue ceilings: a wave64 integer VALU instruction holds its SIMD
 # for 4 cycles (SQ_INSTS_VALU == SQ_ACTIVE_INST_VALU quad-cycles in profiles/r01_pmc), and
 #   DEEP: one message per wave; its SHA-1 chain is 405 VALU per 64-B block (80 rounds x 5 + 5);
-#   WIDE: one message per lane; 717 VALU per 64-B block per wave (SQ_INSTS_VALU of a configs[4]
-#         launch, profiles/r03_wide_crc_pmc: 592 SHA-1 rounds+schedule, 16 byte swaps, 97 CRC-32 ops
-#         from the position tables, loop; 725 with round 3's slicing-by-8; ~630 with SHA-1 only,
-#         from the ISA).
+#   WIDE: one message per lane; VALU per 64-B block per wave from SQ_INSTS_VALU of a configs[4]-sized
+#         launch: WIDE_VALU_FUSED (SHA-1 rounds + schedule, 16 byte swaps, 97 CRC-32 ops from the
+#         position tables, loop; 715.0 with round 4's whole-line loads, profiles/r04_wide_lines/clock.log;
+#         716.5 in round 3, 725 with slicing-by-8) and WIDE_VALU_SHA1 (SHA-1 only: 613.8, profiles/r03_wide_pmc/sha1_only_summary.txt,
+#         1.23552e11 / (3 072 waves x 65 536 blocks)).
+WIDE_VALU_FUSED = 715.0
+WIDE_VALU_SHA1 = 613.8
 CLOCK_HZ = 2.4e9
 N_SIMD = 1024
 VALU_CYC = 4
@@ -556,7 +559,7 @@ def binding_roofline(kernel: str, achieved_gbs: float, concurrent_msgs: int, sha
         model = ("serial SHA-1 chain: each of min(messages, 1024 SIMDs) messages advances one 64-B block per "
                  "405 VALU x 4 cycles at 2.4 GHz (one wave per message)")
     else:
-        per_block = 630 if sha1_only else 717
+        per_block = WIDE_VALU_SHA1 if sha1_only else WIDE_VALU_FUSED
         lanes = min(concurrent_msgs, N_SIMD * 64 * 8)
         ceiling = min(lanes / 64, N_SIMD) * 64 * 64 * CLOCK_HZ / (per_block * VALU_CYC) / 1e9
         model = (f"VALU issue: {per_block} VALU per 64-B block per wave of 64 messages, 4 cycles each, "
@@ -626,12 +629,20 @@ def ingest_leg(args, rank: int, world: int, ctx, device: str, stream, mode: int,
     per_launch_jobs = batches[0].n
     del data, batches
     torch.cuda.empty_cache()
+    # HBM bytes per algorithmic byte of a WIDE launch of this geometry (196 608 distinct 1 MiB
+    # messages), FETCH_SIZE x 2 -- calibrated for WIDE's per-lane access pattern on a known byte count
+    # (tools/microbench/mb_wide_fetch, profiles/r04_fetch/) -- applied to this leg's average launch
+    t = load_traffic("wide_kernel", f"196608x{1 << 20}:sha1+crc32")
+    ratio = None if t is None else t / (196608 * (1 << 20))
     return {"value": round(world * total / wall / GiB, 3), "unit": "GiB/s", "n_gpus": world,
             "scaling": "weak", "bytes_per_gpu": total, "max_rank_wall_s": round(wall, 4), "digests_spot_check": ok,
             "workload": config["workload"],
             "chunks": config["chunks_per_gpu"], "launches": config["launches"], "kernel": "wide_kernel",
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBPS, 5), "kernel_ms": round(kernel_ms, 3)},
+                         "frac": round(achieved / HBM_PEAK_GBPS, 5), "kernel_ms": round(kernel_ms, 3),
+                         "traffic": None if ratio is None else round(ratio * per_launch),
+                         "traffic_per_algorithmic_byte": None if ratio is None else round(ratio, 4),
+                         "algorithmic_bytes_per_launch": int(per_launch)},
             "binding_roofline": binding_roofline("wide_kernel", achieved, per_launch_jobs, args.sha1_only),
             "note": "many concurrent chunks per GPU (configs[4] per-GPU queue); value = all ranks' bytes / the "
                     "slowest rank's wall time; roofline = this rank's kernel; not the headline `value`"}

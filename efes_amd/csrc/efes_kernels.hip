@@ -1347,11 +1347,12 @@ __device__ __forceinline__ void wide_step(const uint32_t (&le)[16], const WideCr
 }
 
 // Whole blocks of one lane's message: block b is hashed (SHA-1 rounds and CRC steps woven
-// together) while blocks b+1 and b+2 are in flight (three 16-word buffers, loop unrolled by
-// three so the buffers keep their registers).  Two phases:
+// together) while the next blocks are in flight (three 16-word buffers, the loop unrolled so the
+// buffers keep their registers).  Two phases:
 //  * uniform: while every lane of the wave still has the blocks being hashed and prefetched
-//    (b+4 < nmin, the wave's shortest message), loads are unconditional and every lane
-//    commits -- no per-lane selects (8 VALU per block fewer than the ragged phase);
+//    (b+5 < nmin, the wave's shortest message), loads are unconditional, a whole 128-B line (two
+//    blocks) at a time, and every lane commits -- no per-lane selects (8 VALU per block fewer
+//    than the ragged phase);
 //  * ragged: up to the wave's longest message (`nmax`, uniform), so the loads stay
 //    unconditional and the compiler's vmcnt waits exact; lanes past their own last block
 //    load a harmless `dummy` block and do not commit.

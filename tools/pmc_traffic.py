@@ -4,8 +4,11 @@
 
 HBM bytes per launch = median over the kernel's dispatches of FETCH_SIZE (KiB) x 1024 x 2:
 on gfx950 FETCH_SIZE reports exactly half the bytes of a wide coalesced streaming read
-(MI355X_MICROARCH.md, section HBM), so it is doubled.  WRITE_SIZE (digests/states, < 200 KiB
-per launch) needs its own pass and is not included.
+(MI355X_MICROARCH.md, section HBM), so it is doubled.  The same x 2 holds for WIDE's per-lane
+pattern (16 B per lane, 64 distinct lines per instruction): calibrated on a known byte count with
+tools/microbench/mb_wide_fetch (profiles/r04_fetch/: FETCH_SIZE x 2 = TCC_EA0_RDREQ x 128 B, no
+32-B requests, and = the bytes read for every shape whose lines are fetched once).  WRITE_SIZE
+(digests/states, < 200 KiB per launch) needs its own pass and is not included.
 """
 import csv
 import json
@@ -26,7 +29,8 @@ def main(path, tag, kernel, workload_key):
         "bytes_per_launch": kib * 1024 * 2,
         "fetch_size_kib_median": kib,
         "dispatches": len(vals),
-        "correction": "FETCH_SIZE (KiB) x 1024 x 2 (gfx950 reports half of a streaming read)",
+        "correction": "FETCH_SIZE (KiB) x 1024 x 2 (gfx950 reports half of a streaming read; the same factor "
+                      "calibrated for WIDE's per-lane pattern, profiles/r04_fetch/)",
         "source": os.path.relpath(path),
     }
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

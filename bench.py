@@ -497,7 +497,8 @@ def make_workload(args, rank: int, world: int, ctx, device: str, stream):
         batches = [DeviceBatch(data.data_ptr(), offs[k::L], sizes[k::L], **kw) for k in range(L)]
         total = int(sizes.sum())
         return data, batches, [int(sizes[k::L].sum()) for k in range(L)], {
-            "workload": f"mixed ChunkSize 64K..64M x {args.mixed_chunks} chunks (BASELINE configs[3])",
+            "workload": f"mixed ChunkSize 64K..64M x {args.mixed_chunks} chunks (BASELINE configs[3]) at random "
+                        f"offsets of a {args.pool_gib} GiB pool",
             "chunks_per_gpu": args.mixed_chunks, "bytes_per_gpu": total, "pool_bytes": pool, "launches": L}
     chunk = 4 << 20
     per_gpu = int(round(args.ingest_tib * (1 << 40) / chunk / 8 * args.ingest_scale))
@@ -741,7 +742,7 @@ def concurrency_leg(args, ctx, device: str, stream):
 
 def mixed_leg(args, rank: int, world: int, ctx, device: str, stream):
     """BASELINE configs[3] beside the metric: 65 536 chunks of the eleven ChunkSize values
-    64K..64M (752 GiB, aliasing a 64 GiB pool), placed by efes_plan_batch (grouped-DEEP parts
+    64K..64M (752 GiB, at random offsets of a 200 GiB pool), placed by efes_plan_batch (grouped-DEEP parts
     on CUs of their own, concurrent with WIDE); one warm-up and one timed step."""
     import argparse as _ap
 
@@ -751,6 +752,10 @@ def mixed_leg(args, rank: int, world: int, ctx, device: str, stream):
 
     a = _ap.Namespace(**vars(args))
     a.workload = "mixed"
+    # 752 GiB of chunks at random offsets of a 200 GiB pool (3.8 chunks over each byte): the 64 GiB
+    # pool of rounds 1-3 (12 over each byte) measured the same, 856.9-858.1 vs 856.7-858.5 GiB/s in
+    # three interleaved pairs (profiles/r04_mixed_pool/ab.log) -- the 64 MiB chains set the makespan
+    a.pool_gib = max(args.pool_gib, 200)
     with torch.cuda.stream(stream):
         data, batches, step_bytes, config = make_workload(a, rank, world, ctx, device, stream)
         for b in batches:

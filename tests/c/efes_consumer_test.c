@@ -15,6 +15,8 @@
  *              compared with the oracle doing the same Writes.
  *   batch   -- efes_hash_submit[_mode] over device buffers from efes_device_alloc (the cgo
  *              path without an allocator of its own), every kernel shape.
+ *   pairs   -- fused MultiWriter digest pairs (ABI 6) driven through every call pattern that splits
+ *              them, from T threads, each sync point against the oracle.
  *   errors  -- errInvalidDigest and the Go panic states surface as error codes.
  * Prints one line "efes_consumer_test ok ..." and exits 0, or names the first mismatch.
  */
@@ -138,6 +140,157 @@ static int test_patch(int threads, int uploads) {
   return !g_fail;
 }
 
+/* ---- pairs: MultiWriter digest pairs that diverge (efes_stream.cpp fused pairs, ABI 6) ------ */
+/* Random scripts of Go-surface calls on one object's two digests, mostly the MultiWriter pattern
+ * (CRC then SHA-1, same buffer) mixed with everything that splits a fused pair: one-digest Writes,
+ * the buffer changed between the two Writes, other lengths, SHA-1 first, empty Writes, Writes larger
+ * than a staging chunk, Reset / UnmarshalText of either, sync points in either order, a member freed
+ * and replaced mid-stream.  Every sync point is compared with the oracle doing the same calls. */
+typedef struct {
+  efes_sha1* s;
+  efes_crc32* c;
+  oracle_sha1 os;
+  oracle_crc32 oc;
+} pair_obj;
+
+static void pair_new(pair_obj* o, int fresh_oracle) {
+  if (efes_sha1_new(g_ctx, &o->s) || efes_crc32_new(g_ctx, &o->c)) FAIL("pair new");
+  if (fresh_oracle) {
+    memset(&o->os, 0, sizeof o->os);
+    oracle_sha1_reset(&o->os);
+    oracle_crc32_reset(&o->oc);
+  }
+}
+
+static void pair_check(pair_obj* o, int sha_first, const char* what, int id, int k) {
+  char st[200], ct[8], ws[200], wc[8];
+  int r1, r2;
+  if (sha_first) {
+    r1 = efes_sha1_marshal_text(o->s, st);
+    r2 = efes_crc32_marshal_text(o->c, ct);
+  } else {
+    r2 = efes_crc32_marshal_text(o->c, ct);
+    r1 = efes_sha1_marshal_text(o->s, st);
+  }
+  oracle_sha1_marshal_text(&o->os, ws);
+  oracle_crc32_marshal_text(&o->oc, wc);
+  if (r1 || r2 || memcmp(st, ws, 200) || memcmp(ct, wc, 8)) FAIL("pair %s thread %d step %d", what, id, k);
+}
+
+static void* pair_worker(void* p) {
+  patch_arg* a = (patch_arg*)p;
+  uint64_t s = 0xA0761D6478BD642Full ^ (uint64_t)(a->id + 1) * 0xE7037ED1A0B428DBull;
+  enum { SIZE = 400000 };
+  uint8_t* buf = malloc(SIZE);
+  for (int u = 0; u < a->uploads && !g_fail; ++u) {
+    oracle_fill_synthetic(buf, SIZE, rnd(&s));
+    pair_obj o;
+    pair_new(&o, 1);
+    for (int k = 0; k < 20 && !g_fail; ++k) {
+      static const size_t ns[] = {1, 55, 64, 4096, 32768, 32768, 40000, 65536};
+      const size_t n = ns[rnd(&s) % 8], off = rnd(&s) % (SIZE - 170000);
+      const uint8_t* q = buf + off;
+      switch (rnd(&s) % 16) {
+        case 0: case 1: case 2: case 3: case 4: /* MultiWriter(f, CRC32, Sha1) */
+          efes_crc32_write(o.c, q, n); oracle_crc32_write(&o.oc, q, n);
+          efes_sha1_write(o.s, q, n); oracle_sha1_write(&o.os, q, n);
+          break;
+        case 5: efes_crc32_write(o.c, q, n); oracle_crc32_write(&o.oc, q, n); break;
+        case 6: efes_sha1_write(o.s, q, n); oracle_sha1_write(&o.os, q, n); break;
+        case 7: { /* the buffer changes between the two Writes (same pointer, other bytes) */
+          efes_crc32_write(o.c, q, n); oracle_crc32_write(&o.oc, q, n);
+          buf[off + rnd(&s) % n] ^= 0x5a;
+          efes_sha1_write(o.s, q, n); oracle_sha1_write(&o.os, q, n);
+          break;
+        }
+        case 8: { /* another length */
+          const size_t m = n > 2 ? n - 1 - rnd(&s) % 2 : 0;
+          efes_crc32_write(o.c, q, n); oracle_crc32_write(&o.oc, q, n);
+          efes_sha1_write(o.s, q, m); oracle_sha1_write(&o.os, q, m);
+          break;
+        }
+        case 9: /* SHA-1 first, then an empty SHA-1 Write */
+          efes_sha1_write(o.s, q, n); oracle_sha1_write(&o.os, q, n);
+          efes_crc32_write(o.c, q, n); oracle_crc32_write(&o.oc, q, n);
+          efes_sha1_write(o.s, q, 0); oracle_sha1_write(&o.os, q, 0);
+          break;
+        case 10: /* a Write larger than a staging chunk */
+          efes_crc32_write(o.c, q, 100000 + n); oracle_crc32_write(&o.oc, q, 100000 + n);
+          efes_sha1_write(o.s, q, 100000 + n); oracle_sha1_write(&o.os, q, 100000 + n);
+          break;
+        case 11: /* Reset of one member with the CRC's Write unconfirmed */
+          efes_crc32_write(o.c, q, n); oracle_crc32_write(&o.oc, q, n);
+          if (rnd(&s) & 1) { efes_crc32_reset(o.c); oracle_crc32_reset(&o.oc); }
+          else { efes_sha1_reset(o.s); oracle_sha1_reset(&o.os); }
+          efes_sha1_write(o.s, q, n); oracle_sha1_write(&o.os, q, n);
+          break;
+        case 12: { /* UnmarshalText of one member (a resumed PATCH) */
+          char t[200];
+          if (rnd(&s) & 1) {
+            oracle_sha1 x; memset(&x, 0, sizeof x); oracle_sha1_reset(&x); oracle_sha1_write(&x, q, 1 + n % 150);
+            oracle_sha1_marshal_text(&x, t);
+            if (efes_sha1_unmarshal_text(o.s, t, 200) || oracle_sha1_unmarshal_text(&o.os, t, 200)) FAIL("pair unmarshal");
+          } else {
+            oracle_crc32 x; oracle_crc32_reset(&x); oracle_crc32_write(&x, q, 77);
+            oracle_crc32_marshal_text(&x, t);
+            if (efes_crc32_unmarshal_text(o.c, t, 8) || oracle_crc32_unmarshal_text(&o.oc, t, 8)) FAIL("pair unmarshal");
+          }
+          break;
+        }
+        case 13: pair_check(&o, (int)(rnd(&s) & 1), "text", a->id, k); break;
+        case 14: { /* a member freed mid-stream (its finalizer) and replaced by one resumed from its text */
+          efes_crc32_write(o.c, q, n); oracle_crc32_write(&o.oc, q, n);
+          char t[200];
+          if (rnd(&s) & 1) {
+            if (efes_crc32_marshal_text(o.c, t)) FAIL("pair crc text");
+            efes_crc32_free(o.c);
+            if (efes_crc32_new(g_ctx, &o.c) || efes_crc32_unmarshal_text(o.c, t, 8)) FAIL("pair crc renew");
+          } else {
+            if (efes_sha1_marshal_text(o.s, t)) FAIL("pair sha text");
+            efes_sha1_free(o.s);
+            if (efes_sha1_new(g_ctx, &o.s) || efes_sha1_unmarshal_text(o.s, t, 200)) FAIL("pair sha renew");
+          }
+          efes_sha1_write(o.s, q, n); oracle_sha1_write(&o.os, q, n);
+          break;
+        }
+        default: { /* Sums in either order */
+          uint8_t d[20], e[20], c[4];
+          const int sf = (int)(rnd(&s) & 1);
+          int r = sf ? efes_sha1_sum(o.s, d) | efes_crc32_sum(o.c, c) : efes_crc32_sum(o.c, c) | efes_sha1_sum(o.s, d);
+          const int orc = oracle_sha1_sum(&o.os, e);
+          const uint32_t oc = oracle_crc32_sum32(&o.oc);
+          const uint8_t ec[4] = {(uint8_t)(oc >> 24), (uint8_t)(oc >> 16), (uint8_t)(oc >> 8), (uint8_t)oc};
+          if (orc == 0 && (r || memcmp(d, e, 20) || memcmp(c, ec, 4))) FAIL("pair sum thread %d step %d", a->id, k);
+          break;
+        }
+      }
+    }
+    pair_check(&o, 1, "end", a->id, -1);
+    efes_sha1_free(o.s);
+    efes_crc32_free(o.c);
+    a->patches++;
+  }
+  free(buf);
+  return NULL;
+}
+
+static int test_pairs(int threads, int scripts) {
+  pthread_t th[64];
+  patch_arg args[64];
+  efes_pair_stats p0, p1;
+  efes_pair_stats_get(&p0);
+  for (int t = 0; t < threads; ++t) {
+    args[t] = (patch_arg){t, scripts, 0, 0};
+    pthread_create(&th[t], NULL, pair_worker, &args[t]);
+  }
+  for (int t = 0; t < threads; ++t) pthread_join(th[t], NULL);
+  efes_pair_stats_get(&p1);
+  printf("pairs: %d threads x %d scripts, %llu pairs bound, %llu settled\n", threads, scripts,
+         (unsigned long long)(p1.pairs - p0.pairs), (unsigned long long)(p1.settles - p0.settles));
+  if (p1.pairs == p0.pairs || p1.settles == p0.settles) FAIL("pairs: no pair bound or settled");
+  return !g_fail;
+}
+
 /* ---- batch: device-resident jobs, every kernel shape -------------------------------------- */
 static int test_batch(void) {
   enum { N = 300 };
@@ -239,7 +392,7 @@ int main(int argc, char** argv) {
     return 1;
   }
   oracle_crc32_init_tables();
-  int ok = test_errors() && test_batch() && test_patch(threads, uploads);
+  int ok = test_errors() && test_batch() && test_patch(threads, uploads) && test_pairs(threads, uploads);
   efes_ctx_destroy(g_ctx);
   if (!ok) return 1;
   printf("efes_consumer_test ok\n");

@@ -13,8 +13,9 @@
 //   * between a sync point and the next Write a digest is PARKED: its state lives on the host
 //     (`sbase` / `cbase`) and it holds no upload;
 //   * a Write (or a Sum of a parked digest) opens an upload from the parked state; when the
-//     queue has no free slot it EVICTS the oldest digest that is not inside a call (hashes what
-//     that one staged, parks it) and takes the slot, or waits for a holder to leave its call;
+//     queue has no free slot it waits for a holder's sync point, EVICTING (hashing what it
+//     staged, parking it) the oldest holder that is not inside a call and has been idle for
+//     EFES_DIGEST_EVICT_MS -- or, once the Write has waited that long, any holder not in a call;
 //   * device faults are latched by Write, which still returns EFES_OK; the sync points report them.
 // Every call holds the digest's mutex (one goroutine per digest, so it is uncontended), which is
 // what lets another thread evict the digest safely between calls.
@@ -74,6 +75,7 @@ struct Digest {
   Fused* fz = nullptr;         // the fused pair this digest is a member of (u/on unused meanwhile)
   const void* cand_p = nullptr;  // a CRC digest whose upload holds exactly its first Write (cand_p, cand_n)
   size_t cand_n = 0;
+  std::atomic<int64_t> last_ns{0};  // end of its last call (eviction prefers long-idle holders)
   bool sha() const { return hashes == EFES_HASH_SHA1; }
   virtual ~Digest() = default;
 };
@@ -97,6 +99,7 @@ struct Fused {
   efes_sha1_state sha_out{};
   efes_crc32_state crc_out{};
   int rc_sha = EFES_OK, rc_crc = EFES_OK;
+  std::atomic<int64_t> last_ns{0};  // end of a member's last call on the pair
 };
 
 }  // namespace efes
@@ -113,6 +116,24 @@ namespace {
 // Process-wide counters (efes_pair_stats_get).
 std::atomic<uint64_t> g_pairs{0}, g_fused_writes{0}, g_fused_bytes{0}, g_settles{0};
 
+int64_t now_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+// Eviction patience: a Write that finds every slot taken first waits for a holder's sync point and
+// evicts only holders idle for this long (a stalled client, an abandoned digest); once it has
+// waited this long itself it evicts the oldest idle holder, active or not (progress).  Evicting
+// active holders at once made every Write of an over-subscribed queue settle another upload and
+// wait for the GPU (EFES_DIGEST_EVICT_MS=0 restores that).
+int64_t evict_patience_ns() {
+  static const int64_t ns = [] {
+    const char* e = getenv("EFES_DIGEST_EVICT_MS");
+    return (e && *e ? strtoll(e, nullptr, 10) : 50) * 1000000ll;
+  }();
+  return ns;
+}
+
 bool fuse_enabled() {
   static const bool on = [] {
     const char* e = getenv("EFES_DIGEST_FUSE");
@@ -121,14 +142,16 @@ bool fuse_enabled() {
   return on;
 }
 
-// Shared queue sizing: EFES_DIGEST_STAGING_MIB of pinned staging (default 256 MiB) in chunks of
-// EFES_DIGEST_CHUNK_KIB (default 64 KiB: 4096 chunks, so up to 4095 digests hold an upload at once).
+// Shared queue sizing: EFES_DIGEST_STAGING_MIB of pinned staging (default 1024 MiB) in chunks of
+// EFES_DIGEST_CHUNK_KIB (default 256 KiB: 4096 chunks, so up to 4095 digests -- or fused pairs --
+// hold an upload at once).  256 KiB chunks: 34.8 against 31.8 GiB/s for 64 KiB with 2 048 uploads
+// in flight (profiles/r04_digest_queue/sweep.log).
 efes_queue* create_digest_queue(efes_ctx* ctx, int* rc) {
-  uint64_t mib = 256, kib = 64;
+  uint64_t mib = 1024, kib = 256;
   if (const char* e = getenv("EFES_DIGEST_STAGING_MIB")) mib = strtoull(e, nullptr, 10);
   if (const char* e = getenv("EFES_DIGEST_CHUNK_KIB")) kib = strtoull(e, nullptr, 10);
   if (mib < 1) mib = 1;
-  if (kib < 4 || kib > 4096) kib = 64;
+  if (kib < 4 || kib > 4096) kib = 256;
   const uint64_t chunk = kib << 10;
   const uint32_t chunks = (uint32_t)((mib << 20) / chunk) < 16 ? 16u : (uint32_t)((mib << 20) / chunk);
   efes_queue* q = nullptr;
@@ -323,6 +346,11 @@ struct Call {
   Digest* d;
   Fused* z = nullptr;
   std::unique_lock<std::mutex> lk, zk;
+  ~Call() {  // still holding d->mu (and z->mu when z is set)
+    const int64_t t = now_ns();
+    d->last_ns.store(t, std::memory_order_relaxed);
+    if (z) z->last_ns.store(t, std::memory_order_relaxed);
+  }
   explicit Call(Digest* dd) : d(dd), lk(dd->mu) {
     uncandidate(d);
     Fused* f = d->fz;
@@ -353,13 +381,16 @@ struct Call {
   }
 };
 
-// Evicts the oldest digest (or fused pair) of ctx's queue that is not inside a call (and is not `self`).
-bool evict_one(efes_ctx* ctx, Digest* self) {
+// Evicts the oldest digest (or fused pair) of ctx's queue that is not inside a call, has been idle
+// for at least min_idle_ns, and is not `self`.
+bool evict_one(efes_ctx* ctx, Digest* self, int64_t min_idle_ns) {
   Digest* victim = nullptr;
   Fused* pair = nullptr;
+  const int64_t horizon = now_ns() - min_idle_ns;
   {
     std::lock_guard<std::mutex> lk(ctx->dreg.mu);
     for (const OpenRef& r : ctx->dreg.open) {
+      if ((r.d ? r.d->last_ns : r.f->last_ns).load(std::memory_order_relaxed) > horizon) continue;
       if (r.d) {
         if (r.d != self && r.d->mu.try_lock()) {
           victim = r.d;
@@ -415,6 +446,7 @@ bool placed_on(const Digest* d, const efes_ctx* c) {
 int acquire(Digest* d) {
   if (d->latched) return d->latched;
   if (d->u) return EFES_OK;
+  const int64_t t0 = now_ns();
   for (;;) {
     efes_ctx* c = place(d);
     int rc = EFES_OK;
@@ -430,10 +462,12 @@ int acquire(Digest* d) {
       return EFES_OK;
     }
     if (!no_slot) return rc;
-    if (evict_one(c, d)) continue;
-    // Every holder is inside a call (writing, or waiting for its own jobs): each of those calls
-    // ends, and its digest becomes evictable.  The timed wait also covers a release that
-    // happened between the scan and the wait.
+    const int64_t patience = evict_patience_ns();
+    if (evict_one(c, d, now_ns() - t0 >= patience ? 0 : patience)) continue;
+    // No holder may be evicted yet: every one is inside a call (writing, or waiting for its own
+    // jobs) or was active within the patience -- each call ends and each holder either reaches its
+    // sync point (releasing the slot) or becomes evictable.  The timed wait also covers a release
+    // that happened between the scan and the wait.
     std::unique_lock<std::mutex> lk(c->dreg.mu);
     c->dreg.released.wait_for(lk, std::chrono::milliseconds(1));
   }
@@ -469,6 +503,7 @@ bool try_bind(Digest* f, const void* p, size_t n) {
   z->u = u;
   z->on = l->on;
   z->pos = l->pos;
+  z->last_ns.store(now_ns(), std::memory_order_relaxed);
   {
     std::lock_guard<std::mutex> lk(l->on->dreg.mu);
     *z->pos = OpenRef{nullptr, z};

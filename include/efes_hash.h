@@ -261,17 +261,21 @@ int efes_queue_get_stats(efes_queue* q, efes_queue_stats* out);
  * own hash, so unchanged Go code -- MultiWriter(f, CRC32, Sha1) in every request goroutine --
  * is batched across all concurrent requests: Write stages into pinned memory and returns,
  * Sum / Sum32 / MarshalText are the sync points.  The shared queue holds
- * EFES_DIGEST_STAGING_MIB (env, default 256) of pinned staging in 64 KiB chunks (an upload slot
- * per chunk but one); a Write blocks while all chunks are in flight.
+ * EFES_DIGEST_STAGING_MIB (env, default 1024) of pinned staging in EFES_DIGEST_CHUNK_KIB (default
+ * 256) chunks -- an upload slot per chunk but one, i.e. 4095 uploads (a fused CRC + SHA-1 pair is
+ * one) per GPU by default; size it to the requests in flight; a Write blocks while all chunks are
+ * in flight.
  *
  * Go's Write never fails (sha1.go:58-79, crc32.go:76-86), and neither does this one for any
  * number of live digests:
  *   - a digest holds an upload slot only between its first Write and its next sync point: every
  *     Sum / Sum32 / MarshalText parks the state on the host and gives the slot back, the next
  *     Write takes one again (so digests that are never freed hold no queue resources);
- *   - a Write (or Sum) that finds every slot taken evicts the oldest digest that is not inside a
- *     call (its staged bytes are hashed, its state parked on the host) and takes its slot; if all
- *     holders are inside calls it waits for one of them -- back-pressure, never EFES_ERR_NOMEM;
+ *   - a Write (or Sum) that finds every slot taken waits for a holder's sync point; it evicts the
+ *     oldest holder that is not inside a call and has been idle for EFES_DIGEST_EVICT_MS (env,
+ *     default 50; a stalled client, an abandoned digest) -- or, once it has itself waited that
+ *     long, the oldest holder not inside a call -- hashing what that one staged and parking its
+ *     state on the host; back-pressure, never EFES_ERR_NOMEM;
  *   - a device or HIP fault during a Write is latched and the Write returns EFES_OK: the next
  *     Sum / Sum32 / MarshalText reports it (MarshalText's error -> HTTP 500, filereceiver.go:94-96).
  * Write returns an error only for bad arguments and for the states on which Go's Write panics

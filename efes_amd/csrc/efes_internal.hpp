@@ -52,6 +52,14 @@ int upload_open_slot(efes_queue* q, uint32_t hashes, const efes_sha1_state* sha1
 int64_t queue_free_slots(efes_queue* q);
 // Test hook behind efes_debug_fault_after: q's k-th launch from now reports a device fault.
 void queue_set_fault_after(efes_queue* q, uint64_t k);
+// efes_queue_create for an owner that can hand idle uploads' partly filled chunks over: then
+// max_uploads may exceed max_chunks.  When writers wait for a chunk while every chunk sits partly
+// filled in uploads (nothing queued or running), the dispatcher thread calls reclaim(arg) -- with
+// no lock held -- which hands over what it can (upload_handover) and returns whether it did.  The
+// digest queue (efes_stream.cpp).
+int queue_create_reclaiming(efes_ctx* ctx, uint64_t chunk_bytes, uint32_t max_chunks, uint32_t max_uploads,
+                            bool (*reclaim)(void*), void* reclaim_arg, efes_queue** out);
+uint64_t queue_reclaims(efes_queue* q);  // reclaim calls so far
 
 // ---- fused digest pairs (efes_stream.cpp on efes_queue.cpp) ----------------------------------
 // io.MultiWriter(f, CRC32, Sha1) (filereceiver.go:208) hands the same bytes to a CRC digest and
@@ -74,6 +82,9 @@ int upload_stage(efes_upload* u, const void* p, size_t n, uint64_t* off);
 int upload_confirm(efes_upload* u, const efes_sha1_state& shadow);
 // Drops the staged bytes of the current chunk from offset `off` on (never handed over).
 void upload_truncate(efes_upload* u, uint64_t off);
+// Hands u's partly filled current chunk to the dispatcher (the caller owns u: no call on it runs);
+// false when u holds none.
+bool upload_handover(efes_upload* u);
 
 // Streaming digests (efes_stream.cpp) that hold an upload of a context's digest queue, oldest
 // first: the candidates for eviction when a digest needs a state slot and none is free.  An

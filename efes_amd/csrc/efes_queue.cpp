@@ -26,6 +26,7 @@
 #include <string.h>
 
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <deque>
 #include <mutex>
@@ -96,6 +97,15 @@ struct efes_queue {
   int fault = EFES_OK;
   uint64_t n_launches = 0, n_jobs = 0, n_bytes = 0;  // efes_queue_get_stats
   uint64_t n_attempts = 0, inject_at = 0;  // test hook (efes_debug_fault_after): launch k faults
+  // max_uploads may exceed the chunks only with a reclaim hook (efes::queue_create_reclaiming):
+  // when writers wait for a chunk and every chunk sits, partly filled, in uploads (nothing queued
+  // or running), the dispatcher calls it -- without mu, holding no lock of the owner layer -- to
+  // hand idle uploads' partly filled chunks over, so no writer waits on chunks nobody hands over.
+  bool (*reclaim)(void*) = nullptr;
+  void* reclaim_arg = nullptr;
+  uint32_t chunk_waiters = 0;      // writers blocked in take_chunk
+  uint64_t n_reclaims = 0;
+  bool starving() const { return reclaim && chunk_waiters > 0 && free_chunks.empty(); }
   // hipEventBlockingSync: the dispatcher sleeps in retire instead of polling the event, so it does
   // not keep a host core busy beside the request threads (receiver within noise either way:
   // profiles/r03_receiver/ab_sync_*.log); EFES_QUEUE_SYNC=spin restores the poll.
@@ -126,10 +136,17 @@ void efes_queue::run() {
   DeviceGuard g(ctx->device);
   std::unique_lock<std::mutex> lk(mu);
   for (;;) {
-    work.wait(lk, [&] { return stop || !pending.empty() || !running.empty(); });
+    work.wait(lk, [&] { return stop || !pending.empty() || !running.empty() || starving(); });
     if (pending.empty()) {
       if (running.empty()) {
         if (stop) return;
+        if (starving()) {  // every chunk is held, partly filled, by an upload: have idle ones handed over
+          ++n_reclaims;
+          lk.unlock();
+          const bool any = reclaim(reclaim_arg);
+          lk.lock();
+          if (!any) work.wait_for(lk, std::chrono::microseconds(200));  // holders busy: look again soon
+        }
         continue;
       }
       Batch b = std::move(running.front());  // nothing new to launch: retire the oldest
@@ -149,6 +166,13 @@ void efes_queue::run() {
     next_half ^= 1;
     std::deque<Pending> later;
     while (!pending.empty()) {
+      // one job-array half holds nchunks jobs: with more uploads than chunks (a reclaiming queue)
+      // the Sums of many uploads could otherwise outnumber it; the rest waits, in order
+      if (b.items.size() >= nchunks) {
+        later.insert(later.end(), pending.begin(), pending.end());
+        pending.clear();
+        break;
+      }
       Pending p = pending.front();
       pending.pop_front();
       if (p.u->in_batch) {
@@ -233,7 +257,12 @@ int enqueue_current(efes_upload* u, std::unique_lock<std::mutex>&, bool even_emp
 // A staging chunk for `u` to fill (q->mu held): waits for a free one.
 int take_chunk(efes_upload* u, std::unique_lock<std::mutex>& lk) {
   efes_queue* q = u->q;
-  q->freed.wait(lk, [&] { return q->fault || !q->free_chunks.empty(); });
+  if (!q->fault && q->free_chunks.empty()) {
+    ++q->chunk_waiters;  // the dispatcher may have to reclaim partly filled chunks (starving())
+    q->work.notify_one();
+    q->freed.wait(lk, [&] { return q->fault || !q->free_chunks.empty(); });
+    --q->chunk_waiters;
+  }
   if (q->fault) return u->latched = q->fault;
   u->cur = (int32_t)q->free_chunks.back();
   q->free_chunks.pop_back();
@@ -304,6 +333,15 @@ int efes_queue_create(efes_ctx* ctx, uint64_t chunk_bytes, uint32_t max_chunks, 
   // Every open upload may hold one partly filled chunk; with max_uploads < max_chunks at least
   // one chunk is always free or queued, so a writer waiting for a chunk always makes progress.
   if (!ctx || !out || max_chunks < 2 || max_uploads == 0 || max_uploads >= max_chunks) return EFES_ERR_ARG;
+  return efes::queue_create_reclaiming(ctx, chunk_bytes, max_chunks, max_uploads, nullptr, nullptr, out);
+}
+
+}  // extern "C"
+
+int efes::queue_create_reclaiming(efes_ctx* ctx, uint64_t chunk_bytes, uint32_t max_chunks, uint32_t max_uploads,
+                                  bool (*reclaim)(void*), void* reclaim_arg, efes_queue** out) {
+  if (!ctx || !out || max_chunks < 2 || max_uploads == 0 || (max_uploads >= max_chunks && !reclaim))
+    return EFES_ERR_ARG;
   *out = nullptr;
   efes_queue* q = new (std::nothrow) efes_queue;
   if (!q) return EFES_ERR_NOMEM;
@@ -311,6 +349,8 @@ int efes_queue_create(efes_ctx* ctx, uint64_t chunk_bytes, uint32_t max_chunks, 
   q->chunk = chunk_bytes ? (chunk_bytes + 63) & ~uint64_t(63) : (uint64_t)1 << 20;
   q->nchunks = max_chunks;
   q->max_uploads = max_uploads;
+  q->reclaim = reclaim;
+  q->reclaim_arg = reclaim_arg;
   const char* ah = getenv("EFES_QUEUE_AHEAD");
   q->ahead = ah && *ah ? strtoull(ah, nullptr, 10) : kAhead;
   if (const char* qs = getenv("EFES_QUEUE_SYNC"); qs && !strcmp(qs, "spin")) q->ev_flags = hipEventDisableTiming;
@@ -339,6 +379,8 @@ int efes_queue_create(efes_ctx* ctx, uint64_t chunk_bytes, uint32_t max_chunks, 
   *out = q;
   return EFES_OK;
 }
+
+extern "C" {
 
 void efes_queue_destroy(efes_queue* q) {
   if (!q) return;
@@ -643,6 +685,18 @@ int upload_confirm(efes_upload* u, const efes_sha1_state& shadow) {
     pace(u, lk);
   }
   return u->latched;
+}
+
+bool upload_handover(efes_upload* u) {
+  std::unique_lock<std::mutex> lk(u->q->mu);
+  if (u->cur < 0 || u->fill == 0) return false;
+  enqueue_current(u, lk);
+  return true;
+}
+
+uint64_t queue_reclaims(efes_queue* q) {
+  std::lock_guard<std::mutex> lk(q->mu);
+  return q->n_reclaims;
 }
 
 void upload_truncate(efes_upload* u, uint64_t off) {

@@ -142,20 +142,34 @@ bool fuse_enabled() {
   return on;
 }
 
+bool reclaim_chunks(void* arg);
+
 // Shared queue sizing: EFES_DIGEST_STAGING_MIB of pinned staging (default 1024 MiB) in chunks of
-// EFES_DIGEST_CHUNK_KIB (default 256 KiB: 4096 chunks, so up to 4095 digests -- or fused pairs --
-// hold an upload at once).  256 KiB chunks: 34.8 against 31.8 GiB/s for 64 KiB with 2 048 uploads
-// in flight (profiles/r04_digest_queue/sweep.log).
+// EFES_DIGEST_CHUNK_KIB (default 256 KiB: 4096 chunks; 256 KiB chunks ran 34.8 against 31.8 GiB/s
+// for 64 KiB with 2 048 uploads in flight, profiles/r04_digest_queue/sweep.log), and
+// EFES_DIGEST_SLOTS upload slots (default 65 536: 256 B of pinned state each).  A digest or fused
+// pair holds a slot from its first Write to its sync point; with more slots than chunks, the
+// dispatcher hands idle holders' partly filled chunks over when writers wait for one
+// (reclaim_chunks), so requests in flight are bounded by the slots, not by the staging -- with one
+// slot per chunk, 8 192 uploads in flight on 4 095 slots ran at 0.9 GiB/s, every Write evicting
+// (settling) another upload.  EFES_DIGEST_SLOTS below the chunks gives round 3's queue (slots =
+// min(EFES_DIGEST_SLOTS, chunks - 1), no reclaim).
 efes_queue* create_digest_queue(efes_ctx* ctx, int* rc) {
-  uint64_t mib = 1024, kib = 256;
+  uint64_t mib = 1024, kib = 256, slots = 65536;
   if (const char* e = getenv("EFES_DIGEST_STAGING_MIB")) mib = strtoull(e, nullptr, 10);
   if (const char* e = getenv("EFES_DIGEST_CHUNK_KIB")) kib = strtoull(e, nullptr, 10);
+  if (const char* e = getenv("EFES_DIGEST_SLOTS")) slots = strtoull(e, nullptr, 10);
   if (mib < 1) mib = 1;
   if (kib < 4 || kib > 4096) kib = 256;
+  if (slots < 1) slots = 1;
+  if (slots > (1u << 22)) slots = 1u << 22;
   const uint64_t chunk = kib << 10;
   const uint32_t chunks = (uint32_t)((mib << 20) / chunk) < 16 ? 16u : (uint32_t)((mib << 20) / chunk);
   efes_queue* q = nullptr;
-  *rc = efes_queue_create(ctx, chunk, chunks, chunks - 1, &q);
+  if (slots >= chunks)
+    *rc = efes::queue_create_reclaiming(ctx, chunk, chunks, (uint32_t)slots, reclaim_chunks, ctx, &q);
+  else
+    *rc = efes_queue_create(ctx, chunk, chunks, (uint32_t)slots, &q);
   if (*rc == EFES_OK && ctx->fault_after) efes::queue_set_fault_after(q, ctx->fault_after);
   return *rc == EFES_OK ? q : nullptr;
 }
@@ -380,6 +394,31 @@ struct Call {
     return ::leave(d, f, sync, zk);
   }
 };
+
+// The digest queue's reclaim hook (run by its dispatcher thread, which holds no digest or pair
+// lock): every chunk sits partly filled in an upload while writers wait for one, so each holder
+// that is not inside a call hands its partly filled chunk over (hashed like a full one, then
+// freed).  A fused pair with an unconfirmed leader Write keeps its chunk: its follower's Write
+// comes next.  Returns whether anything was handed over.
+bool reclaim_chunks(void* arg) {
+  efes_ctx* ctx = static_cast<efes_ctx*>(arg);
+  std::vector<OpenRef> got;
+  {
+    std::lock_guard<std::mutex> lk(ctx->dreg.mu);
+    got.reserve(ctx->dreg.open.size());
+    for (const OpenRef& r : ctx->dreg.open)
+      if (r.d ? r.d->mu.try_lock() : r.f->mu.try_lock()) got.push_back(r);
+  }
+  // Locked holders cannot be freed, parked or settled meanwhile (each needs the lock we hold).
+  bool any = false;
+  for (const OpenRef& r : got) {
+    efes_upload* u = r.d ? r.d->u : (r.f->open ? nullptr : r.f->u);
+    if (u && efes::upload_handover(u)) any = true;
+    if (r.d) r.d->mu.unlock();
+    else r.f->mu.unlock();
+  }
+  return any;
+}
 
 // Evicts the oldest digest (or fused pair) of ctx's queue that is not inside a call, has been idle
 // for at least min_idle_ns, and is not `self`.

@@ -3,7 +3,8 @@
 Go's sha1digest.Write / crc32digest.Write never fail (sha1.go:58-79, crc32.go:76-86), and
 filereceiver.go creates two fresh digests per PATCH (fileinfo.go:20-27, filereceiver.go:180-182)
 that only the garbage collector frees.  These tests hold that contract with a deliberately tiny
-digest queue (EFES_DIGEST_STAGING_MIB=1: 16 staging chunks, 15 upload slots):
+digest queue (EFES_DIGEST_STAGING_MIB=1: 16 staging chunks) with 15 upload slots (eviction) and
+with 65 536 (chunk reclaim by the dispatcher):
   * 200 PATCHes, each through a NEW FileInfo that is never freed until the end;
   * more digests written-but-not-synced at once than there are slots (eviction), from 16 threads;
   * a device fault in the middle of a Write stream: Write still returns len(p), the sync points
@@ -32,11 +33,16 @@ def gpu():
     return dict(efes=efes_amd, hashing=hashing)
 
 
-@pytest.fixture
-def small_ctx(gpu, monkeypatch):
-    """A fresh context whose digest queue (created at its first digest Write) has 15 upload slots."""
+@pytest.fixture(params=["evict", "reclaim"])
+def small_ctx(gpu, monkeypatch, request):
+    """A fresh context whose digest queue (created at its first digest Write) has 16 staging chunks and
+    either 15 upload slots (round 3's queue: a Write that finds no slot evicts an idle holder) or
+    65 536 (round 4's default: more uploads than chunks, the dispatcher has idle holders hand their
+    partly filled chunks over when writers wait for one)."""
     monkeypatch.setenv("EFES_DIGEST_STAGING_MIB", "1")
+    monkeypatch.setenv("EFES_DIGEST_SLOTS", "15" if request.param == "evict" else "65536")
     ctx = gpu["hashing"].Context(0)
+    ctx.slots = 15 if request.param == "evict" else 65536
     yield ctx
     ctx.close()
 
@@ -116,7 +122,7 @@ def test_200_patches_new_fileinfo_each_never_freed(gpu, small_ctx, oracle):
                 assert fi.digest.crc32.sum32() == zlib.crc32(data)
                 assert fi.digest.sha1.marshal_text().decode() == expect[o].sha.marshal_text()
     st = pool1.stats(0)
-    assert st.max_uploads == 15 and st.free_uploads == 15  # every digest is parked after its sync point
+    assert st.max_uploads == small_ctx.slots and st.free_uploads == small_ctx.slots  # all parked after their sync points
     # every PATCH's MultiWriter pair was fused: each body byte staged and hashed ONCE (two separate
     # digests hashed it twice until round 3)
     total = sum(len(b) for bs in bodies.values() for b in bs)
@@ -129,8 +135,9 @@ def test_200_patches_new_fileinfo_each_never_freed(gpu, small_ctx, oracle):
 
 def test_more_unsynced_digests_than_slots_evict(gpu, small_ctx, oracle):
     """48 digests written to and NOT synced (as a failed saveFile abandons them to the GC) on a queue
-    with 15 upload slots: every Write succeeds -- the oldest idle holder is evicted (its staged
-    bytes hashed, its state parked on the host) -- and each digest, synced later, equals the oracle."""
+    with 16 staging chunks: every Write succeeds -- with 15 slots the oldest idle holder is evicted
+    (its staged bytes hashed, its state parked on the host), with 65 536 the idle holders' partly
+    filled chunks are handed over -- and each digest, synced later, equals the oracle."""
     hashing = gpu["hashing"]
     n = 48
     digests = [hashing.Digest(small_ctx) for _ in range(n)]

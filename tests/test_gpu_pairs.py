@@ -218,11 +218,14 @@ def test_diverging_pairs_random_scripts(gpu, oracle, oracle_lib):
     assert d["pairs"] > 100 and d["settles"] > 50, d
 
 
-def test_diverging_pairs_16_threads_small_queue(gpu, oracle, oracle_lib, monkeypatch):
-    """The same scripts from 16 threads on a context whose digest queue has 15 upload slots (pairs
-    evicted and settled between their members' calls, mid-Write included), plus a pool over two
+@pytest.mark.parametrize("slots", ["15", "65536"])
+def test_diverging_pairs_16_threads_small_queue(gpu, oracle, oracle_lib, monkeypatch, slots):
+    """The same scripts from 16 threads on a context whose digest queue has 16 staging chunks and 15
+    upload slots (pairs evicted and settled between their members' calls, mid-Write included) or
+    65 536 (partly filled chunks of idle pairs handed over by the dispatcher), plus a pool over two
     contexts: every text and digest equals the oracle's, nothing deadlocks."""
     monkeypatch.setenv("EFES_DIGEST_STAGING_MIB", "1")
+    monkeypatch.setenv("EFES_DIGEST_SLOTS", slots)
     h = gpu["hashing"]
     gpu = dict(gpu, oracle_lib=oracle_lib)
     small = h.Context(0)

@@ -138,15 +138,22 @@ void efes_queue::run() {
   for (;;) {
     work.wait(lk, [&] { return stop || !pending.empty() || !running.empty() || starving(); });
     if (pending.empty()) {
+      if (starving() && !stop) {
+        // Writers wait for a chunk and none is free: every chunk not in a launch sits partly filled
+        // in an upload.  Have the idle holders hand theirs over, so the next launch is assembled
+        // while the running one finishes.
+        ++n_reclaims;
+        lk.unlock();
+        const bool any = reclaim(reclaim_arg);
+        lk.lock();
+        if (any) continue;
+        if (running.empty()) {  // holders busy, nothing to retire: look again soon
+          work.wait_for(lk, std::chrono::microseconds(200));
+          continue;
+        }
+      }
       if (running.empty()) {
         if (stop) return;
-        if (starving()) {  // every chunk is held, partly filled, by an upload: have idle ones handed over
-          ++n_reclaims;
-          lk.unlock();
-          const bool any = reclaim(reclaim_arg);
-          lk.lock();
-          if (!any) work.wait_for(lk, std::chrono::microseconds(200));  // holders busy: look again soon
-        }
         continue;
       }
       Batch b = std::move(running.front());  // nothing new to launch: retire the oldest

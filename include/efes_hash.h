@@ -262,9 +262,11 @@ int efes_queue_get_stats(efes_queue* q, efes_queue_stats* out);
  * is batched across all concurrent requests: Write stages into pinned memory and returns,
  * Sum / Sum32 / MarshalText are the sync points.  The shared queue holds
  * EFES_DIGEST_STAGING_MIB (env, default 1024) of pinned staging in EFES_DIGEST_CHUNK_KIB (default
- * 256) chunks -- an upload slot per chunk but one, i.e. 4095 uploads (a fused CRC + SHA-1 pair is
- * one) per GPU by default; size it to the requests in flight; a Write blocks while all chunks are
- * in flight.
+ * 256) chunks and EFES_DIGEST_SLOTS (default 65536) upload slots: a digest (a fused CRC + SHA-1 pair
+ * is one) holds a slot from its first Write to its sync point; when writers wait for a chunk and
+ * every chunk sits partly filled in idle uploads, the queue's dispatcher has those handed over.  A
+ * Write blocks while all chunks are in flight.  EFES_DIGEST_SLOTS below the chunk count gives one
+ * slot per chunk at most (no hand-over; a Write evicts instead, below).
  *
  * Go's Write never fails (sha1.go:58-79, crc32.go:76-86), and neither does this one for any
  * number of live digests:

@@ -98,9 +98,9 @@ struct efes_queue {
   uint64_t n_launches = 0, n_jobs = 0, n_bytes = 0;  // efes_queue_get_stats
   uint64_t n_attempts = 0, inject_at = 0;  // test hook (efes_debug_fault_after): launch k faults
   // max_uploads may exceed the chunks only with a reclaim hook (efes::queue_create_reclaiming):
-  // when writers wait for a chunk and every chunk sits, partly filled, in uploads (nothing queued
-  // or running), the dispatcher calls it -- without mu, holding no lock of the owner layer -- to
-  // hand idle uploads' partly filled chunks over, so no writer waits on chunks nobody hands over.
+  // when writers wait for a chunk, none is free and nothing is queued, the dispatcher calls it --
+  // without mu, holding no lock of the owner layer -- to have idle uploads hand their partly
+  // filled chunks over, so no writer waits on chunks that nobody would hand over.
   bool (*reclaim)(void*) = nullptr;
   void* reclaim_arg = nullptr;
   uint32_t chunk_waiters = 0;      // writers blocked in take_chunk

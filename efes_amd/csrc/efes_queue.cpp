@@ -677,7 +677,15 @@ int upload_stage(efes_upload* u, const void* p, size_t n, uint64_t* off) {
     if (int rc = take_chunk(u, lk)) return rc;
     u->fill = 0;
   }
-  copy_to_staging(q->h_slab + (size_t)u->cur * q->chunk + u->fill, static_cast<const uint8_t*>(p), n);
+  // The follower's memcmp reads these bytes right back: EFES_PAIR_STAGE=cached stages them with
+  // ordinary stores (A/B against the streaming stores of every other Write).
+  static const bool cached = [] {
+    const char* e = getenv("EFES_PAIR_STAGE");
+    return e && !strcmp(e, "cached");
+  }();
+  uint8_t* dst = q->h_slab + (size_t)u->cur * q->chunk + u->fill;
+  if (cached) memcpy(dst, p, n);
+  else copy_to_staging(dst, static_cast<const uint8_t*>(p), n);
   *off = u->fill;
   u->fill += n;
   return EFES_OK;

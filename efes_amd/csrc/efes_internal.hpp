@@ -76,8 +76,9 @@ void upload_fuse(efes_upload* u, const efes_sha1_state& sha, const efes_sha1_sta
 // u keeps only `hashes` from now on (a member of a fused pair left it).
 void upload_keep(efes_upload* u, uint32_t hashes);
 // Stages n <= chunk bytes into u's current chunk WITHOUT handing them over (a current chunk without
-// room is handed over first); *off = their offset in the current chunk.  No host replay.
-int upload_stage(efes_upload* u, const void* p, size_t n, uint64_t* off);
+// room is handed over first); *off = their offset in the current chunk.  No host replay.  cached:
+// ordinary stores (the bytes are read back on this core next), else streaming stores.
+int upload_stage(efes_upload* u, const void* p, size_t n, uint64_t* off, bool cached);
 // The follower matched the staged bytes: its replayed Go state; a full chunk is handed over.
 int upload_confirm(efes_upload* u, const efes_sha1_state& shadow);
 // Drops the staged bytes of the current chunk from offset `off` on (never handed over).

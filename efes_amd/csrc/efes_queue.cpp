@@ -664,7 +664,7 @@ void upload_keep(efes_upload* u, uint32_t hashes) {
   }
 }
 
-int upload_stage(efes_upload* u, const void* p, size_t n, uint64_t* off) {
+int upload_stage(efes_upload* u, const void* p, size_t n, uint64_t* off, bool cached) {
   if (u->latched) return u->latched;
   efes_queue* q = u->q;
   if (u->cur >= 0 && u->fill + n > q->chunk) {  // no room: hand the (matched) chunk over first
@@ -677,13 +677,6 @@ int upload_stage(efes_upload* u, const void* p, size_t n, uint64_t* off) {
     if (int rc = take_chunk(u, lk)) return rc;
     u->fill = 0;
   }
-  // The follower's memcmp reads these bytes right back, so the leader stages them with ordinary
-  // stores and the compare hits the cache (profiles/r04_pair_stage_ab: 43.5-43.7 GiB/s against
-  // 35.2-39.8 with the streaming stores every other Write uses). EFES_PAIR_STAGE=stream = A/B.
-  static const bool cached = [] {
-    const char* e = getenv("EFES_PAIR_STAGE");
-    return !(e && !strcmp(e, "stream"));
-  }();
   uint8_t* dst = q->h_slab + (size_t)u->cur * q->chunk + u->fill;
   if (cached) memcpy(dst, p, n);
   else copy_to_staging(dst, static_cast<const uint8_t*>(p), n);

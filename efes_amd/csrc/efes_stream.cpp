@@ -50,6 +50,7 @@
 #include <chrono>
 #include <new>
 #include <unordered_map>
+#include <utility>
 #include <vector>
 
 #include "efes_internal.hpp"
@@ -100,6 +101,10 @@ struct Fused {
   efes_crc32_state crc_out{};
   int rc_sha = EFES_OK, rc_crc = EFES_OK;
   std::atomic<int64_t> last_ns{0};  // end of a member's last call on the pair
+  // EFES_PAIR_STAGE=scratch: the leader's open Write waits here instead of in the upload
+  uint8_t* scratch = nullptr;
+  size_t scratch_cap = 0;
+  ~Fused() { free(scratch); }
 };
 
 }  // namespace efes
@@ -132,6 +137,58 @@ int64_t evict_patience_ns() {
     return (e && *e ? strtoll(e, nullptr, 10) : 50) * 1000000ll;
   }();
   return ns;
+}
+
+// Where the leader's Write waits for the follower's (EFES_PAIR_STAGE):
+//   cached  -- staged in the upload with ordinary stores, so the follower's memcmp hits the cache
+//              (default; 43.5-43.7 against 35.2-39.8 GiB/s for `stream`, profiles/r04_pair_stage_ab);
+//   stream  -- staged with the streaming stores of every other Write: the memcmp reads DRAM;
+//   scratch -- copied into a cache-hot per-thread scratch buffer; the follower's Write compares
+//              against it and then stages with streaming stores (no read-for-ownership of staging).
+enum class PairStage { kCached, kStream, kScratch };
+PairStage pair_stage() {
+  static const PairStage m = [] {
+    const char* e = getenv("EFES_PAIR_STAGE");
+    if (e && !strcmp(e, "stream")) return PairStage::kStream;
+    if (e && !strcmp(e, "scratch")) return PairStage::kScratch;
+    return PairStage::kCached;
+  }();
+  return m;
+}
+
+// Scratch buffers for PairStage::kScratch: a few per thread, reused last-in first-out so the one a
+// leader Write copies into is still in this core's cache when the follower's Write (normally on
+// the same thread, right after) compares against it.  A buffer may be returned on another thread.
+struct ScratchCache {
+  std::vector<std::pair<uint8_t*, size_t>> bufs;
+  ~ScratchCache() {
+    for (auto& b : bufs) free(b.first);
+  }
+};
+thread_local ScratchCache t_scratch;
+
+uint8_t* scratch_get(size_t n, size_t* cap) {
+  auto& v = t_scratch.bufs;
+  for (size_t i = v.size(); i-- > 0;)
+    if (v[i].second >= n) {
+      const auto b = v[i];
+      v.erase(v.begin() + (ptrdiff_t)i);
+      *cap = b.second;
+      return b.first;
+    }
+  const size_t c = (n + 65535) & ~(size_t)65535;
+  uint8_t* p = static_cast<uint8_t*>(aligned_alloc(64, c));
+  *cap = p ? c : 0;
+  return p;
+}
+
+void scratch_put(uint8_t* p, size_t cap) {
+  auto& v = t_scratch.bufs;
+  if (v.size() >= 4) {
+    free(v.front().first);
+    v.erase(v.begin());
+  }
+  v.emplace_back(p, cap);
 }
 
 bool fuse_enabled() {
@@ -251,6 +308,20 @@ void park(Digest* d) {
 }
 
 // ---- fused pairs --------------------------------------------------------------------------------
+// The leader's open Write: in its scratch buffer, or staged in the upload's current chunk.
+const uint8_t* pending(const Fused* z) { return z->scratch ? z->scratch : efes::upload_staged(z->u, z->ooff); }
+
+// Gives the leader's open Write up (z->mu held).
+void drop_pending(Fused* z) {
+  if (z->scratch) {
+    scratch_put(z->scratch, z->scratch_cap);
+    z->scratch = nullptr;
+  } else {
+    efes::upload_truncate(z->u, z->ooff);
+  }
+  z->open = false;
+}
+
 // Settles the pair (z->mu held): every matched byte is hashed into both states, the leader's
 // unmatched Write (if any) into the CRC state alone; both states are left for the members to pick
 // up and the upload is given back.
@@ -259,10 +330,9 @@ void settle(Fused* z) {
   if (!u) return;
   std::vector<uint8_t> tail;
   if (z->open) {  // the leader's bytes the follower never matched: hashed for the leader only
-    const uint8_t* t = efes::upload_staged(u, z->ooff);
+    const uint8_t* t = pending(z);
     tail.assign(t, t + z->on_bytes);
-    efes::upload_truncate(u, z->ooff);
-    z->open = false;
+    drop_pending(z);
   }
   efes_sha1_state s = efes::upload_shadow(u);
   efes_crc32_state c{};
@@ -334,12 +404,14 @@ int leave(Digest* d, Fused* z, bool sync, std::unique_lock<std::mutex>& zk) {
       if (rc != EFES_OK && d->latched == EFES_OK) d->latched = rc;
     }
     efes::upload_keep(u, EFES_HASH_CRC32);
+    if (z->open && z->scratch) {  // the leader's open Write is its own: into the (now CRC-only) upload
+      uint64_t off = 0;
+      (void)efes::upload_stage(u, z->scratch, z->on_bytes, &off, false);  // a fault is latched in u
+      drop_pending(z);
+    }
     z->follow_in = false;
   } else {
-    if (z->open) {
-      efes::upload_truncate(u, z->ooff);
-      z->open = false;
-    }
+    if (z->open) drop_pending(z);
     if (sync) {
       efes_crc32_state c{};
       rc = efes_upload_state(u, nullptr, &c);
@@ -398,8 +470,8 @@ struct Call {
 // The digest queue's reclaim hook (run by its dispatcher thread, which holds no digest or pair
 // lock): every chunk sits partly filled in an upload while writers wait for one, so each holder
 // that is not inside a call hands its partly filled chunk over (hashed like a full one, then
-// freed).  A fused pair with an unconfirmed leader Write keeps its chunk: its follower's Write
-// comes next.  Returns whether anything was handed over.
+// freed).  A fused pair with an unconfirmed leader Write staged in its chunk keeps the chunk: its
+// follower's Write comes next.  Returns whether anything was handed over.
 bool reclaim_chunks(void* arg) {
   efes_ctx* ctx = static_cast<efes_ctx*>(arg);
   std::vector<OpenRef> got;
@@ -412,7 +484,7 @@ bool reclaim_chunks(void* arg) {
   // Locked holders cannot be freed, parked or settled meanwhile (each needs the lock we hold).
   bool any = false;
   for (const OpenRef& r : got) {
-    efes_upload* u = r.d ? r.d->u : (r.f->open ? nullptr : r.f->u);
+    efes_upload* u = r.d ? r.d->u : (r.f->open && !r.f->scratch ? nullptr : r.f->u);
     if (u && efes::upload_handover(u)) any = true;
     if (r.d) r.d->mu.unlock();
     else r.f->mu.unlock();
@@ -567,12 +639,18 @@ int digest_write(Digest* d, const void* p, size_t n) {
     if (d->sha()) {  // the follower: the leader's Write of the same bytes is staged already
       if (n == 0) {
         if (efes::upload_shadow(u).nx != 64) return EFES_OK;  // an empty Write changes nothing
-      } else if (z->open && p == z->op && n == z->on_bytes &&
-                 memcmp(efes::upload_staged(u, z->ooff), p, n) == 0) {
+      } else if (z->open && p == z->op && n == z->on_bytes && memcmp(pending(z), p, n) == 0) {
         efes_sha1_state sh = efes::upload_shadow(u);
         if (efes::replay_write(&sh, static_cast<const uint8_t*>(p), n) == EFES_OK) {
-          z->open = false;
-          (void)efes::upload_confirm(u, sh);  // a fault is latched in the upload for the sync points
+          // a fault is latched in the upload for the sync points
+          if (z->scratch) {  // the bytes are this Write's: staged now, with streaming stores
+            drop_pending(z);
+            uint64_t off = 0;
+            if (efes::upload_stage(u, p, n, &off, false) == EFES_OK) (void)efes::upload_confirm(u, sh);
+          } else {
+            z->open = false;
+            (void)efes::upload_confirm(u, sh);
+          }
           g_fused_writes.fetch_add(1, std::memory_order_relaxed);
           g_fused_bytes.fetch_add(n, std::memory_order_relaxed);
           return EFES_OK;
@@ -581,14 +659,28 @@ int digest_write(Digest* d, const void* p, size_t n) {
     } else {  // the leader: stage, and wait for the follower's Write to match
       if (n == 0) return EFES_OK;  // crc32.go:76-86 of nothing
       if (!z->open && n <= efes::upload_chunk_bytes(u)) {
-        uint64_t off = 0;
-        if (efes::upload_stage(u, p, n, &off) == EFES_OK) {
-          z->open = true;
-          z->op = p;
-          z->on_bytes = n;
-          z->ooff = off;
-        }  // else the fault is latched in the upload
-        return EFES_OK;
+        const PairStage m = pair_stage();
+        if (m == PairStage::kScratch) {
+          size_t cap = 0;
+          if (uint8_t* b = scratch_get(n, &cap)) {
+            memcpy(b, p, n);
+            z->scratch = b;
+            z->scratch_cap = cap;
+            z->open = true;
+            z->op = p;
+            z->on_bytes = n;
+            return EFES_OK;
+          }  // no memory for a scratch buffer: split
+        } else {
+          uint64_t off = 0;
+          if (efes::upload_stage(u, p, n, &off, m == PairStage::kCached) == EFES_OK) {
+            z->open = true;
+            z->op = p;
+            z->on_bytes = n;
+            z->ooff = off;
+          }  // else the fault is latched in the upload
+          return EFES_OK;
+        }
       }
     }
     c.split();  // the Writes diverged: both continue alone

@@ -79,6 +79,9 @@ void upload_keep(efes_upload* u, uint32_t hashes);
 // room is handed over first); *off = their offset in the current chunk.  No host replay.  cached:
 // ordinary stores (the bytes are read back on this core next), else streaming stores.
 int upload_stage(efes_upload* u, const void* p, size_t n, uint64_t* off, bool cached);
+// upload_stage with streaming stores that checks the bytes against `ref` in the same pass: they
+// count as staged (fill advances, *off set) only when *same.
+int upload_stage_if_same(efes_upload* u, const void* p, const void* ref, size_t n, uint64_t* off, bool* same);
 // The follower matched the staged bytes: its replayed Go state; a full chunk is handed over.
 int upload_confirm(efes_upload* u, const efes_sha1_state& shadow);
 // Drops the staged bytes of the current chunk from offset `off` on (never handed over).

@@ -323,6 +323,42 @@ void copy_to_staging(uint8_t* dst, const uint8_t* src, size_t n) {
   _mm_sfence();
 }
 
+// copy_to_staging that also compares src with ref (same length) in the same pass; returns whether
+// they are equal.  The copy is complete either way.
+bool copy_to_staging_if_same(uint8_t* dst, const uint8_t* src, const uint8_t* ref, size_t n) {
+  if (n < 4096) {
+    memcpy(dst, src, n);
+    return memcmp(src, ref, n) == 0;
+  }
+  const size_t head = (16 - (reinterpret_cast<uintptr_t>(dst) & 15)) & 15;
+  bool same = memcmp(src, ref, head) == 0;
+  memcpy(dst, src, head);
+  dst += head;
+  src += head;
+  ref += head;
+  n -= head;
+  __m128i diff = _mm_setzero_si128();
+  size_t i = 0;
+  for (; i + 64 <= n; i += 64) {
+    const __m128i a = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i));
+    const __m128i b = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 16));
+    const __m128i c = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 32));
+    const __m128i d = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 48));
+    diff = _mm_or_si128(diff, _mm_or_si128(_mm_xor_si128(a, _mm_loadu_si128(reinterpret_cast<const __m128i*>(ref + i))),
+                                           _mm_xor_si128(b, _mm_loadu_si128(reinterpret_cast<const __m128i*>(ref + i + 16)))));
+    diff = _mm_or_si128(diff, _mm_or_si128(_mm_xor_si128(c, _mm_loadu_si128(reinterpret_cast<const __m128i*>(ref + i + 32))),
+                                           _mm_xor_si128(d, _mm_loadu_si128(reinterpret_cast<const __m128i*>(ref + i + 48)))));
+    _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i), a);
+    _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 16), b);
+    _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 32), c);
+    _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 48), d);
+  }
+  same = same && memcmp(src + i, ref + i, n - i) == 0;
+  memcpy(dst + i, src + i, n - i);
+  _mm_sfence();
+  return same && _mm_movemask_epi8(_mm_cmpeq_epi8(diff, _mm_setzero_si128())) == 0xFFFF;
+}
+
 int wait_idle(efes_upload* u) {
   efes_queue* q = u->q;
   std::unique_lock<std::mutex> lk(q->mu);
@@ -682,6 +718,30 @@ int upload_stage(efes_upload* u, const void* p, size_t n, uint64_t* off, bool ca
   else copy_to_staging(dst, static_cast<const uint8_t*>(p), n);
   *off = u->fill;
   u->fill += n;
+  return EFES_OK;
+}
+
+int upload_stage_if_same(efes_upload* u, const void* p, const void* ref, size_t n, uint64_t* off, bool* same) {
+  *same = false;
+  if (u->latched) return u->latched;
+  efes_queue* q = u->q;
+  if (u->cur >= 0 && u->fill + n > q->chunk) {  // no room: hand the (matched) chunk over first
+    std::unique_lock<std::mutex> lk(q->mu);
+    enqueue_current(u, lk);
+    pace(u, lk);
+  }
+  if (u->cur < 0) {
+    std::unique_lock<std::mutex> lk(q->mu);
+    if (int rc = take_chunk(u, lk)) return rc;
+    u->fill = 0;
+  }
+  // bytes past `fill` are never handed over, so a mismatch leaves nothing behind
+  *same = copy_to_staging_if_same(q->h_slab + (size_t)u->cur * q->chunk + u->fill, static_cast<const uint8_t*>(p),
+                                  static_cast<const uint8_t*>(ref), n);
+  if (*same) {
+    *off = u->fill;
+    u->fill += n;
+  }
   return EFES_OK;
 }
 

@@ -143,8 +143,9 @@ int64_t evict_patience_ns() {
 //   cached  -- staged in the upload with ordinary stores, so the follower's memcmp hits the cache
 //              (default; 43.5-43.7 against 35.2-39.8 GiB/s for `stream`, profiles/r04_pair_stage_ab);
 //   stream  -- staged with the streaming stores of every other Write: the memcmp reads DRAM;
-//   scratch -- copied into a cache-hot per-thread scratch buffer; the follower's Write compares
-//              against it and then stages with streaming stores (no read-for-ownership of staging).
+//   scratch -- copied into a cache-hot per-thread scratch buffer; the follower's Write stages with
+//              streaming stores while comparing against it in the same pass (no read-for-ownership
+//              of the staging lines, no second pass over the bytes).
 enum class PairStage { kCached, kStream, kScratch };
 PairStage pair_stage() {
   static const PairStage m = [] {
@@ -639,21 +640,27 @@ int digest_write(Digest* d, const void* p, size_t n) {
     if (d->sha()) {  // the follower: the leader's Write of the same bytes is staged already
       if (n == 0) {
         if (efes::upload_shadow(u).nx != 64) return EFES_OK;  // an empty Write changes nothing
-      } else if (z->open && p == z->op && n == z->on_bytes && memcmp(pending(z), p, n) == 0) {
+      } else if (z->open && p == z->op && n == z->on_bytes) {
         efes_sha1_state sh = efes::upload_shadow(u);
         if (efes::replay_write(&sh, static_cast<const uint8_t*>(p), n) == EFES_OK) {
-          // a fault is latched in the upload for the sync points
-          if (z->scratch) {  // the bytes are this Write's: staged now, with streaming stores
-            drop_pending(z);
+          bool same = false;
+          if (z->scratch) {  // staged now (streaming stores), compared with the leader's copy in the same pass
             uint64_t off = 0;
-            if (efes::upload_stage(u, p, n, &off, false) == EFES_OK) (void)efes::upload_confirm(u, sh);
-          } else {
+            if (efes::upload_stage_if_same(u, p, z->scratch, n, &off, &same) != EFES_OK) {
+              drop_pending(z);  // the fault is latched in the upload for the sync points
+              return EFES_OK;
+            }
+            if (same) drop_pending(z);
+          } else if (memcmp(pending(z), p, n) == 0) {
+            same = true;
             z->open = false;
-            (void)efes::upload_confirm(u, sh);
           }
-          g_fused_writes.fetch_add(1, std::memory_order_relaxed);
-          g_fused_bytes.fetch_add(n, std::memory_order_relaxed);
-          return EFES_OK;
+          if (same) {
+            (void)efes::upload_confirm(u, sh);  // a fault is latched in the upload for the sync points
+            g_fused_writes.fetch_add(1, std::memory_order_relaxed);
+            g_fused_bytes.fetch_add(n, std::memory_order_relaxed);
+            return EFES_OK;
+          }
         }
       }
     } else {  // the leader: stage, and wait for the follower's Write to match

@@ -8,7 +8,7 @@ cd "${GRAFT_REPO_ROOT:?}" || exit 1
 O=gpurun_out/${1:-r04_pair_stage_ab}
 mkdir -p "$O"
 if [ "${SKIP_TESTS:-0}" != 1 ]; then
-  EFES_PAIR_STAGE=scratch timeout -k 10 600 python -u -m pytest tests/test_gpu_pairs.py tests/test_gpu_go_surface.py \
+  EFES_PAIR_STAGE=scratch timeout -k 10 600 python -u -m pytest tests/test_gpu_pairs.py tests/test_gpu_go_surface.py tests/test_gpu_consumer.py \
     tests/test_gpu_boundary.py -x -q --timeout 200 --timeout-method thread > "$O/tests_scratch.log" 2>&1 || { tail -30 "$O/tests_scratch.log"; exit 1; }
   tail -1 "$O/tests_scratch.log"
 fi

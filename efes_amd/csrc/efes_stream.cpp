@@ -140,19 +140,21 @@ int64_t evict_patience_ns() {
 }
 
 // Where the leader's Write waits for the follower's (EFES_PAIR_STAGE):
-//   cached  -- staged in the upload with ordinary stores, so the follower's memcmp hits the cache
-//              (default; 43.5-43.7 against 35.2-39.8 GiB/s for `stream`, profiles/r04_pair_stage_ab);
-//   stream  -- staged with the streaming stores of every other Write: the memcmp reads DRAM;
-//   scratch -- copied into a cache-hot per-thread scratch buffer; the follower's Write stages with
-//              streaming stores while comparing against it in the same pass (no read-for-ownership
-//              of the staging lines, no second pass over the bytes).
+//   scratch -- (default) copied into a cache-hot per-thread scratch buffer; the follower's Write
+//              stages with streaming stores while comparing against it in the same pass (no
+//              read-for-ownership of the staging lines, no second pass over the bytes);
+//   cached  -- staged in the upload with ordinary stores, so the follower's memcmp hits the cache;
+//   stream  -- staged with the streaming stores of every other Write: the memcmp reads DRAM.
+// Interleaved on one box (profiles/r04_pair_stage_ab2/ab.log): scratch 46.8-47.7, cached 45.9-46.4,
+// stream 46.3-47.5 GiB/s, efes_upload 48.9-49.3; on another (r04_pair_stage_ab) stream ran 35.2-39.8
+// against cached 43.5-43.7.
 enum class PairStage { kCached, kStream, kScratch };
 PairStage pair_stage() {
   static const PairStage m = [] {
     const char* e = getenv("EFES_PAIR_STAGE");
     if (e && !strcmp(e, "stream")) return PairStage::kStream;
-    if (e && !strcmp(e, "scratch")) return PairStage::kScratch;
-    return PairStage::kCached;
+    if (e && !strcmp(e, "cached")) return PairStage::kCached;
+    return PairStage::kScratch;
   }();
   return m;
 }

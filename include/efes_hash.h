@@ -298,7 +298,8 @@ typedef struct efes_crc32 efes_crc32;
  *     UnmarshalText / free of one, an eviction) splits the pair: every confirmed byte is in both
  *     states, an unconfirmed CRC Write in the CRC state only, and both go on alone.
  * Every digest therefore hashes exactly the bytes of its own Writes, in order, whatever the caller
- * does; only the speed depends on the pattern.  EFES_DIGEST_FUSE=0 (env) disables binding.
+ * does; only the speed depends on the pattern.  EFES_DIGEST_FUSE=0 (env) disables binding;
+ * EFES_PAIR_STAGE=scratch|cached|stream (env) picks where a leader's Write waits.
  * Process-wide counters: */
 typedef struct efes_pair_stats {
     uint64_t pairs;         /* CRC + SHA-1 digests bound to one upload */

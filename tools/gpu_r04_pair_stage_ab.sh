@@ -1,7 +1,7 @@
 #!/bin/bash
-# Round 4: where the fused pair's leader Write waits for the follower's (EFES_PAIR_STAGE): staged
-# with ordinary stores (cached, the default), with streaming stores (stream), or in a per-thread
-# scratch buffer with the follower staging by streaming stores (scratch).  The pair / Go-surface /
+# Round 4: where the fused pair's leader Write waits for the follower's (EFES_PAIR_STAGE): in a
+# per-thread scratch buffer with the follower staging by streaming stores (scratch, the default since
+# this A/B), staged with ordinary stores (cached), or staged with streaming stores (stream).  The pair / Go-surface /
 # boundary tests run under the scratch mode first; then the bench configuration, interleaved.
 set -uo pipefail
 cd "${GRAFT_REPO_ROOT:?}" || exit 1

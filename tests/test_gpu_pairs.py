@@ -112,7 +112,10 @@ def _script(gpu, oracle, rng: random.Random, steps: int, ctx=None, pool=None, ta
             o.sha_write(buf, off, n)
         elif op == "mutated":  # same pointer, the buffer changed between the two Writes
             o.crc_write(buf, off, n)
-            buf[off + rng.randrange(n)] ^= 1 + rng.randrange(255)
+            # the first / last 64 bytes or anywhere: the fused compare-and-stage has a head, a
+            # 64-byte body loop and a tail
+            at = rng.choice([rng.randrange(min(n, 64)), n - 1 - rng.randrange(min(n, 64)), rng.randrange(n)])
+            buf[off + at] ^= 1 + rng.randrange(255)
             o.sha_write(buf, off, n)
         elif op == "other_len":
             o.crc_write(buf, off, n)

@@ -14,7 +14,10 @@ pattern must fuse completely: every byte hashed once (queue byte counter = body 
 """
 import ctypes
 import hashlib
+import os
 import random
+import subprocess
+import sys
 import threading
 import zlib
 
@@ -288,3 +291,34 @@ def test_member_freed_or_reset_mid_stream(gpu, oracle, oracle_lib):
             o.check_texts(True, "crc first")
         del o
     assert h  # the module stays imported while digests are freed
+
+
+_MODE_CHILD = r"""
+import random, sys
+sys.path[:0] = [{root!r}, {tests!r}]
+from oracle import oracle
+oracle.build()
+import efes_amd
+from efes_amd import _lib, hashing
+import test_gpu_pairs as T
+gpu = dict(efes=efes_amd, hashing=hashing, lib=_lib.lib(), check=_lib.check, oracle_lib=oracle.lib())
+s0 = hashing.pair_stats()
+for seed in range(40):
+    T._script(gpu, oracle, random.Random(500 + seed), 24, tag="seed %d" % seed)
+s1 = hashing.pair_stats()
+d = {{k: s1[k] - s0[k] for k in s0}}
+assert d["pairs"] > 10 and d["settles"] > 5, d
+print("ok", d)
+"""
+
+
+@pytest.mark.parametrize("mode", ["cached", "stream"])
+def test_diverging_pairs_other_staging_modes(gpu, mode):
+    """The random scripts under the non-default EFES_PAIR_STAGE modes (read once per process, so in
+    a child process): the leader's Write staged in the upload with ordinary or streaming stores
+    instead of waiting in a scratch buffer.  Every text and digest equals the oracle's."""
+    tests = os.path.dirname(os.path.abspath(__file__))
+    code = _MODE_CHILD.format(root=os.path.dirname(tests), tests=tests)
+    r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, EFES_PAIR_STAGE=mode),
+                       capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0 and "ok" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])

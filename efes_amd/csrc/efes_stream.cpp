@@ -45,6 +45,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include <atomic>
 #include <chrono>
@@ -118,12 +119,26 @@ using efes::OpenRef;
 
 namespace {
 
-// Process-wide counters (efes_pair_stats_get).
-std::atomic<uint64_t> g_pairs{0}, g_fused_writes{0}, g_fused_bytes{0}, g_settles{0};
+// Process-wide counters (efes_pair_stats_get), sharded by thread: every fused Write counts, and one
+// shared cache line bounced between 32 request threads cost more than the pair check at small Writes.
+struct alignas(64) PairCounters {
+  std::atomic<uint64_t> pairs{0}, fused_writes{0}, fused_bytes{0}, settles{0};
+};
+constexpr uint32_t kCounterShards = 64;
+PairCounters g_counters[kCounterShards];
 
+PairCounters& counters() {
+  static std::atomic<uint32_t> next{0};
+  thread_local PairCounters* mine = &g_counters[next.fetch_add(1, std::memory_order_relaxed) % kCounterShards];
+  return *mine;
+}
+
+// Idle times for eviction (a 50 ms patience) need no better than the coarse clock's few ms, and it
+// costs a fraction of a precise read on every call.
 int64_t now_ns() {
-  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
-      .count();
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC_COARSE, &ts);
+  return (int64_t)ts.tv_sec * 1000000000ll + ts.tv_nsec;
 }
 
 // Eviction patience: a Write that finds every slot taken first waits for a holder's sync point and
@@ -356,7 +371,7 @@ void settle(Fused* z) {
   z->u = nullptr;
   z->on = nullptr;
   z->settled = true;
-  g_settles.fetch_add(1, std::memory_order_relaxed);
+  counters().settles.fetch_add(1, std::memory_order_relaxed);
 }
 
 // d stops being a member of z (z->mu held through zk, released here); the last member frees z.
@@ -626,9 +641,10 @@ bool try_bind(Digest* f, const void* p, size_t n) {
   l->on = nullptr;
   l->fz = z;
   f->fz = z;
-  g_pairs.fetch_add(1, std::memory_order_relaxed);
-  g_fused_writes.fetch_add(1, std::memory_order_relaxed);
-  g_fused_bytes.fetch_add(n, std::memory_order_relaxed);
+  PairCounters& k = counters();
+  k.pairs.fetch_add(1, std::memory_order_relaxed);
+  k.fused_writes.fetch_add(1, std::memory_order_relaxed);
+  k.fused_bytes.fetch_add(n, std::memory_order_relaxed);
   return true;
 }
 
@@ -659,8 +675,9 @@ int digest_write(Digest* d, const void* p, size_t n) {
           }
           if (same) {
             (void)efes::upload_confirm(u, sh);  // a fault is latched in the upload for the sync points
-            g_fused_writes.fetch_add(1, std::memory_order_relaxed);
-            g_fused_bytes.fetch_add(n, std::memory_order_relaxed);
+            PairCounters& k = counters();
+            k.fused_writes.fetch_add(1, std::memory_order_relaxed);
+            k.fused_bytes.fetch_add(n, std::memory_order_relaxed);
             return EFES_OK;
           }
         }
@@ -814,10 +831,13 @@ int efes_pool_stats(efes_pool* p, uint32_t i, efes_queue_stats* out) {
 
 int efes_pair_stats_get(efes_pair_stats* out) {
   if (!out) return EFES_ERR_ARG;
-  out->pairs = g_pairs.load(std::memory_order_relaxed);
-  out->fused_writes = g_fused_writes.load(std::memory_order_relaxed);
-  out->fused_bytes = g_fused_bytes.load(std::memory_order_relaxed);
-  out->settles = g_settles.load(std::memory_order_relaxed);
+  memset(out, 0, sizeof *out);
+  for (const PairCounters& k : g_counters) {
+    out->pairs += k.pairs.load(std::memory_order_relaxed);
+    out->fused_writes += k.fused_writes.load(std::memory_order_relaxed);
+    out->fused_bytes += k.fused_bytes.load(std::memory_order_relaxed);
+    out->settles += k.settles.load(std::memory_order_relaxed);
+  }
   return EFES_OK;
 }
 

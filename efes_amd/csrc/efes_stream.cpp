@@ -177,22 +177,34 @@ PairStage pair_stage() {
 // Scratch buffers for PairStage::kScratch: a few per thread, reused last-in first-out so the one a
 // leader Write copies into is still in this core's cache when the follower's Write (normally on
 // the same thread, right after) compares against it.  A buffer may be returned on another thread.
-struct ScratchCache {
-  std::vector<std::pair<uint8_t*, size_t>> bufs;
-  ~ScratchCache() {
-    for (auto& b : bufs) free(b.first);
+// The per-thread slots are trivially destructible, so a digest call made while the thread is being
+// torn down (after the reaper below has freed the slots) still finds valid storage: it frees the
+// buffer instead of caching it.
+struct ScratchBuf {
+  uint8_t* p;
+  size_t cap;
+};
+constexpr uint32_t kScratchPerThread = 4;
+thread_local ScratchBuf t_scratch[kScratchPerThread];
+thread_local uint32_t t_nscratch = 0;
+thread_local bool t_scratch_reaped = false;
+struct ScratchReaper {
+  ~ScratchReaper() {
+    for (uint32_t i = 0; i < t_nscratch; ++i) free(t_scratch[i].p);
+    t_nscratch = 0;
+    t_scratch_reaped = true;
   }
 };
-thread_local ScratchCache t_scratch;
+thread_local ScratchReaper t_scratch_reaper;
 
 uint8_t* scratch_get(size_t n, size_t* cap) {
-  auto& v = t_scratch.bufs;
-  for (size_t i = v.size(); i-- > 0;)
-    if (v[i].second >= n) {
-      const auto b = v[i];
-      v.erase(v.begin() + (ptrdiff_t)i);
-      *cap = b.second;
-      return b.first;
+  for (uint32_t i = t_nscratch; i-- > 0;)
+    if (t_scratch[i].cap >= n) {
+      const ScratchBuf b = t_scratch[i];
+      for (uint32_t k = i + 1; k < t_nscratch; ++k) t_scratch[k - 1] = t_scratch[k];
+      --t_nscratch;
+      *cap = b.cap;
+      return b.p;
     }
   const size_t c = (n + 65535) & ~(size_t)65535;
   uint8_t* p = static_cast<uint8_t*>(aligned_alloc(64, c));
@@ -201,12 +213,17 @@ uint8_t* scratch_get(size_t n, size_t* cap) {
 }
 
 void scratch_put(uint8_t* p, size_t cap) {
-  auto& v = t_scratch.bufs;
-  if (v.size() >= 4) {
-    free(v.front().first);
-    v.erase(v.begin());
+  if (t_scratch_reaped) {
+    free(p);
+    return;
   }
-  v.emplace_back(p, cap);
+  (void)&t_scratch_reaper;  // registers the reaper for this thread
+  if (t_nscratch == kScratchPerThread) {
+    free(t_scratch[0].p);
+    for (uint32_t k = 1; k < kScratchPerThread; ++k) t_scratch[k - 1] = t_scratch[k];
+    --t_nscratch;
+  }
+  t_scratch[t_nscratch++] = ScratchBuf{p, cap};
 }
 
 bool fuse_enabled() {

@@ -82,6 +82,11 @@ int upload_stage(efes_upload* u, const void* p, size_t n, uint64_t* off, bool ca
 // upload_stage with streaming stores that checks the bytes against `ref` in the same pass: they
 // count as staged (fill advances, *off set) only when *same.
 int upload_stage_if_same(efes_upload* u, const void* p, const void* ref, size_t n, uint64_t* off, bool* same);
+// Bytes the current staging chunk can still take (a whole chunk when there is none or it is full).
+uint64_t upload_room(const efes_upload* u);
+// Replaces the host-replayed Go state (x/nx/len) with one that differs at most in the stale bytes
+// x[nx:] (a Write hashed in pieces gets the single Write's replay back).
+void upload_set_shadow(efes_upload* u, const efes_sha1_state& shadow);
 // The follower matched the staged bytes: its replayed Go state; a full chunk is handed over.
 int upload_confirm(efes_upload* u, const efes_sha1_state& shadow);
 // Drops the staged bytes of the current chunk from offset `off` on (never handed over).

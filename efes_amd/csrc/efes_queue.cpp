@@ -674,6 +674,13 @@ efes_sha1_state upload_shadow(const efes_upload* u) { return u->shadow; }
 // The caller owns the upload as its writer (cur/fill need no lock, as in efes_upload_write).
 uint64_t upload_chunk_bytes(const efes_upload* u) { return u->q->chunk; }
 
+uint64_t upload_room(const efes_upload* u) {
+  const uint64_t c = u->q->chunk;
+  return u->cur >= 0 && u->fill < c ? c - u->fill : c;
+}
+
+void upload_set_shadow(efes_upload* u, const efes_sha1_state& shadow) { u->shadow = shadow; }
+
 bool upload_holds_only(efes_upload* u, size_t n) {
   std::lock_guard<std::mutex> lk(u->q->mu);
   return !u->latched && u->inflight == 0 && u->queued == 0 && u->cur >= 0 && u->fill == n && !u->fold_sum;

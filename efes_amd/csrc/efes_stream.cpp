@@ -78,8 +78,12 @@ struct Digest {
   const void* cand_p = nullptr;  // a CRC digest whose upload holds exactly its first Write (cand_p, cand_n)
   size_t cand_n = 0;
   std::atomic<int64_t> last_ns{0};  // end of its last call (eviction prefers long-idle holders)
+  // EFES_PAIR_STAGE=scratch: a CRC digest's first Write on a fresh upload waits here, as the
+  // candidate, until a SHA-1 digest binds to it or the digest's next call stages it
+  uint8_t* defer = nullptr;
+  size_t defer_cap = 0, defer_n = 0;
   bool sha() const { return hashes == EFES_HASH_SHA1; }
-  virtual ~Digest() = default;
+  virtual ~Digest() { free(defer); }
 };
 
 // One upload shared by a CRC digest (the leader: MultiWriter writes it first) and a SHA-1 digest
@@ -105,6 +109,7 @@ struct Fused {
   // EFES_PAIR_STAGE=scratch: the leader's open Write waits here instead of in the upload
   uint8_t* scratch = nullptr;
   size_t scratch_cap = 0;
+  size_t conf = 0;  // bytes of the open scratch Write the follower has confirmed (staged in pieces)
   ~Fused() { free(scratch); }
 };
 
@@ -185,6 +190,7 @@ struct ScratchBuf {
   size_t cap;
 };
 constexpr uint32_t kScratchPerThread = 4;
+constexpr size_t kScratchKeepMax = 1u << 20;  // larger buffers (Writes of more than 1 MiB) are not kept
 thread_local ScratchBuf t_scratch[kScratchPerThread];
 thread_local uint32_t t_nscratch = 0;
 thread_local bool t_scratch_reaped = false;
@@ -213,7 +219,7 @@ uint8_t* scratch_get(size_t n, size_t* cap) {
 }
 
 void scratch_put(uint8_t* p, size_t cap) {
-  if (t_scratch_reaped) {
+  if (t_scratch_reaped || cap > kScratchKeepMax) {
     free(p);
     return;
   }
@@ -343,8 +349,12 @@ void park(Digest* d) {
 }
 
 // ---- fused pairs --------------------------------------------------------------------------------
-// The leader's open Write: in its scratch buffer, or staged in the upload's current chunk.
-const uint8_t* pending(const Fused* z) { return z->scratch ? z->scratch : efes::upload_staged(z->u, z->ooff); }
+// The leader's open Write (what of it the follower has not confirmed): in its scratch buffer, or
+// staged in the upload's current chunk.
+const uint8_t* pending(const Fused* z) {
+  return z->scratch ? z->scratch + z->conf : efes::upload_staged(z->u, z->ooff);
+}
+size_t pending_n(const Fused* z) { return z->on_bytes - z->conf; }
 
 // Gives the leader's open Write up (z->mu held).
 void drop_pending(Fused* z) {
@@ -355,6 +365,7 @@ void drop_pending(Fused* z) {
     efes::upload_truncate(z->u, z->ooff);
   }
   z->open = false;
+  z->conf = 0;
 }
 
 // Settles the pair (z->mu held): every matched byte is hashed into both states, the leader's
@@ -366,7 +377,7 @@ void settle(Fused* z) {
   std::vector<uint8_t> tail;
   if (z->open) {  // the leader's bytes the follower never matched: hashed for the leader only
     const uint8_t* t = pending(z);
-    tail.assign(t, t + z->on_bytes);
+    tail.assign(t, t + pending_n(z));
     drop_pending(z);
   }
   efes_sha1_state s = efes::upload_shadow(u);
@@ -440,8 +451,7 @@ int leave(Digest* d, Fused* z, bool sync, std::unique_lock<std::mutex>& zk) {
     }
     efes::upload_keep(u, EFES_HASH_CRC32);
     if (z->open && z->scratch) {  // the leader's open Write is its own: into the (now CRC-only) upload
-      uint64_t off = 0;
-      (void)efes::upload_stage(u, z->scratch, z->on_bytes, &off, false);  // a fault is latched in u
+      (void)efes_upload_write(u, pending(z), pending_n(z));  // a fault is latched in u
       drop_pending(z);
     }
     z->follow_in = false;
@@ -460,9 +470,27 @@ int leave(Digest* d, Fused* z, bool sync, std::unique_lock<std::mutex>& zk) {
   return rc;
 }
 
+int acquire(Digest* d);
+
+// A CRC digest's deferred first Write (no SHA-1 digest bound to it before the digest's next call)
+// goes into an upload of its own -- or is dropped when the digest's state is being replaced.
+// d->mu held.
+void undefer(Digest* d, bool keep) {
+  uint8_t* b = d->defer;
+  if (!b) return;
+  d->defer = nullptr;
+  if (keep) {
+    int rc = acquire(d);
+    if (rc == EFES_OK) rc = efes_upload_write(d->u, b, d->defer_n);
+    if (rc != EFES_OK && d->latched == EFES_OK) d->latched = rc;
+  }
+  scratch_put(b, d->defer_cap);
+}
+
 // One call on a digest: d->mu, and for a member of a live pair the pair's mutex too (`z` set).  A
 // member of a settled pair picks up its state, one whose partner left takes the upload over; both
-// are alone again (`z` null).  A CRC digest's candidacy ends with its next call.
+// are alone again (`z` null).  A CRC digest's candidacy ends with its next call, and its deferred
+// first Write is staged (keep) or dropped (the call replaces the state: free, Reset, UnmarshalText).
 struct Call {
   Digest* d;
   Fused* z = nullptr;
@@ -472,8 +500,9 @@ struct Call {
     d->last_ns.store(t, std::memory_order_relaxed);
     if (z) z->last_ns.store(t, std::memory_order_relaxed);
   }
-  explicit Call(Digest* dd) : d(dd), lk(dd->mu) {
+  explicit Call(Digest* dd, bool keep = true) : d(dd), lk(dd->mu) {
     uncandidate(d);
+    undefer(d, keep);
     Fused* f = d->fz;
     if (!f) return;
     zk = std::unique_lock<std::mutex>(f->mu);
@@ -619,32 +648,85 @@ int acquire(Digest* d) {
   }
 }
 
-// A parked SHA-1 digest's Write (p, n) joins the CRC digest whose fresh upload holds exactly the
-// same bytes (MultiWriter(f, CRC32, Sha1) just wrote them there): the upload keeps both hashes
-// from now on.  f->mu held, f parked and not fused.
-bool try_bind(Digest* f, const void* p, size_t n) {
+void count_fused(size_t n) {
+  PairCounters& k = counters();
+  k.fused_writes.fetch_add(1, std::memory_order_relaxed);
+  k.fused_bytes.fetch_add(n, std::memory_order_relaxed);
+}
+
+enum class Bind { kNo, kDone, kPending };
+
+// A parked SHA-1 digest's Write (p, n) joins the CRC digest whose last Write was the same (p, n)
+// (MultiWriter(f, CRC32, Sha1) just made it).  c.d is the SHA-1 digest (its mutex held), parked and
+// not fused.
+//   scratch mode: the CRC digest's Write is deferred in its scratch buffer.  The pair opens ONE
+//     upload keeping both hashes (SHA-1 from the SHA-1 digest's parked state, CRC from the CRC
+//     digest's) and the deferred bytes become the pair's open leader Write, which the SHA-1 Write
+//     then confirms as a follower (kPending: c.z and c.zk are set);
+//   other modes: the CRC digest's fresh upload holds exactly those bytes, staged and not handed
+//     over; they are compared here and the upload keeps both hashes from now on (kDone).
+Bind try_bind(Call& c, const uint8_t* p, size_t n) {
+  Digest* f = c.d;
   Digest* l;
   {
     CandShard& s = shard_of(p);
     std::lock_guard<std::mutex> lk(s.mu);
     auto it = s.m.find(p);
-    if (it == s.m.end()) return false;
+    if (it == s.m.end()) return Bind::kNo;
     l = it->second;
     // try_lock: l's owner may be inside a call (or freeing l, which first takes l->mu and then
     // this shard's lock): then no bind.  Holding the shard lock keeps l alive until we hold l->mu.
-    if (l == f || l->cand_n != n || !l->mu.try_lock()) return false;
+    if (l == f || l->cand_n != n || !l->mu.try_lock()) return Bind::kNo;
     s.m.erase(it);
     l->cand_p = nullptr;
   }
   std::unique_lock<std::mutex> llk(l->mu, std::adopt_lock);
-  if (l->fz || !l->u || l->latched || l->sha() || !placed_on(f, l->on)) return false;
+  if (l->fz || l->latched || l->sha()) return Bind::kNo;
+  if (l->defer) {
+    if (l->u || l->defer_n != n) return Bind::kNo;
+    efes_ctx* on = place(l);
+    if (!placed_on(f, on)) return Bind::kNo;
+    int rc = EFES_OK;
+    efes_queue* q = efes::stream_queue(on, &rc);
+    if (!q) return Bind::kNo;
+    bool no_slot = false;
+    efes_upload* u = nullptr;
+    if (efes::upload_open_slot(q, EFES_HASH_SHA1 | EFES_HASH_CRC32, &f->sbase, &l->cbase, &u, &no_slot) != EFES_OK)
+      return Bind::kNo;  // no free slot: both go on alone (l stages its Write at its next call)
+    Fused* z = new (std::nothrow) Fused;
+    if (!z) {
+      efes_upload_close(u);
+      return Bind::kNo;
+    }
+    // the pair is locked before an evictor or the reclaim hook can find it in the registry
+    c.zk = std::unique_lock<std::mutex>(z->mu);
+    c.z = z;
+    z->u = u;
+    z->on = on;
+    z->open = true;  // l's deferred Write is the pair's open leader Write
+    z->op = p;
+    z->on_bytes = n;
+    z->scratch = l->defer;
+    z->scratch_cap = l->defer_cap;
+    l->defer = nullptr;
+    z->last_ns.store(now_ns(), std::memory_order_relaxed);
+    {
+      std::lock_guard<std::mutex> lk(on->dreg.mu);
+      z->pos = on->dreg.open.insert(on->dreg.open.end(), OpenRef{nullptr, z});
+    }
+    l->fz = z;
+    f->fz = z;
+    counters().pairs.fetch_add(1, std::memory_order_relaxed);
+    return Bind::kPending;
+  }
+  if (!l->u || !placed_on(f, l->on)) return Bind::kNo;
   efes_upload* u = l->u;
-  if (!efes::upload_holds_only(u, n)) return false;
-  if (memcmp(efes::upload_staged(u, 0), p, n) != 0) return false;  // the staged bytes ARE this Write
+  if (!efes::upload_holds_only(u, n)) return Bind::kNo;
+  if (memcmp(efes::upload_staged(u, 0), p, n) != 0) return Bind::kNo;  // the staged bytes ARE this Write
   efes_sha1_state shadow = f->sbase;
-  if (efes::replay_write(&shadow, static_cast<const uint8_t*>(p), n) != EFES_OK) return false;  // Go panics: alone
+  if (efes::replay_write(&shadow, p, n) != EFES_OK) return Bind::kNo;  // Go panics: alone
   Fused* z = new (std::nothrow) Fused;
-  if (!z) return false;
+  if (!z) return Bind::kNo;
   efes::upload_fuse(u, f->sbase, shadow);
   z->u = u;
   z->on = l->on;
@@ -658,83 +740,138 @@ bool try_bind(Digest* f, const void* p, size_t n) {
   l->on = nullptr;
   l->fz = z;
   f->fz = z;
-  PairCounters& k = counters();
-  k.pairs.fetch_add(1, std::memory_order_relaxed);
-  k.fused_writes.fetch_add(1, std::memory_order_relaxed);
-  k.fused_bytes.fetch_add(n, std::memory_order_relaxed);
+  counters().pairs.fetch_add(1, std::memory_order_relaxed);
+  count_fused(n);
+  return Bind::kDone;
+}
+
+// The leader's (CRC) Write in a live pair: it waits for the follower's.  False: the pair splits.
+bool lead(Call& c, const uint8_t* p, size_t n) {
+  Fused* z = c.z;
+  if (n == 0) return true;    // crc32.go:76-86 of nothing
+  if (z->open) return false;  // the follower never confirmed the previous one
+  const PairStage m = pair_stage();
+  if (m == PairStage::kScratch) {
+    size_t cap = 0;
+    uint8_t* b = scratch_get(n, &cap);
+    if (!b) return false;  // no memory for a scratch buffer
+    memcpy(b, p, n);
+    z->scratch = b;
+    z->scratch_cap = cap;
+    z->conf = 0;
+    z->open = true;
+    z->op = p;
+    z->on_bytes = n;
+    return true;
+  }
+  if (n > efes::upload_chunk_bytes(z->u)) return false;
+  uint64_t off = 0;
+  if (efes::upload_stage(z->u, p, n, &off, m == PairStage::kCached) == EFES_OK) {
+    z->open = true;
+    z->op = p;
+    z->on_bytes = n;
+    z->ooff = off;
+  }  // else the fault is latched in the upload
   return true;
+}
+
+// The follower's (SHA-1) Write in a live pair: the leader's open Write must be the same (p, n) and
+// the same bytes.  True: done.  False: the pair splits and the follower writes p[0, n) alone -- after
+// a scratch Write confirmed in part, p / n are advanced past the confirmed bytes and *whole is the
+// Go state after the single Write (the caller's pieces would leave other stale bytes in x[nx:]).
+bool follow(Call& c, const uint8_t*& p, size_t& n, efes_sha1_state* whole, bool* split_mid) {
+  Fused* z = c.z;
+  efes_upload* u = z->u;
+  if (n == 0) return efes::upload_shadow(u).nx != 64;  // an empty Write changes nothing (else: alone)
+  if (!z->open || p != z->op || n != z->on_bytes) return false;
+  const efes_sha1_state s0 = efes::upload_shadow(u);
+  efes_sha1_state sh = s0;
+  if (efes::replay_write(&sh, p, n) != EFES_OK) return false;  // Go panics: alone
+  if (!z->scratch) {  // staged by the leader: compare
+    if (memcmp(pending(z), p, n) != 0) return false;
+    z->open = false;
+    (void)efes::upload_confirm(u, sh);  // a fault is latched in the upload for the sync points
+    count_fused(n);
+    return true;
+  }
+  // Staged now, piece by piece (a Write larger than the room left in the chunk spans several), with
+  // streaming stores compared with the leader's copy in the same pass.  Each piece is confirmed with
+  // the Go state after it (its x[:nx] is what a later job continues from), the last one with the
+  // single Write's state.
+  efes_sha1_state ps = s0;
+  size_t done = 0;
+  while (done < n) {
+    const size_t piece = (size_t)std::min<uint64_t>(n - done, efes::upload_room(u));
+    bool same = false;
+    uint64_t off = 0;
+    if (efes::upload_stage_if_same(u, p + done, z->scratch + done, piece, &off, &same) != EFES_OK) {
+      drop_pending(z);  // the fault is latched in the upload for the sync points
+      return true;
+    }
+    if (!same) break;
+    (void)efes::replay_write(&ps, p + done, piece);
+    done += piece;
+    z->conf = done;
+    (void)efes::upload_confirm(u, done < n ? ps : sh);
+  }
+  if (done == n) {
+    drop_pending(z);
+    count_fused(n);
+    return true;
+  }
+  if (done) {
+    *whole = sh;
+    *split_mid = true;
+    p += done;
+    n -= done;
+  }
+  return false;
 }
 
 // Write(p): Go's never fails except where it panics (nx > 64 -> EFES_ERR_STATE).  Other errors
 // are latched for the next sync point.
-int digest_write(Digest* d, const void* p, size_t n) {
-  if (!d || (!p && n)) return EFES_ERR_ARG;
+int digest_write(Digest* d, const void* p0, size_t n0) {
+  if (!d || (!p0 && n0)) return EFES_ERR_ARG;
   Call c(d);
-  if (Fused* z = c.z) {
-    efes_upload* u = z->u;
-    if (d->sha()) {  // the follower: the leader's Write of the same bytes is staged already
-      if (n == 0) {
-        if (efes::upload_shadow(u).nx != 64) return EFES_OK;  // an empty Write changes nothing
-      } else if (z->open && p == z->op && n == z->on_bytes) {
-        efes_sha1_state sh = efes::upload_shadow(u);
-        if (efes::replay_write(&sh, static_cast<const uint8_t*>(p), n) == EFES_OK) {
-          bool same = false;
-          if (z->scratch) {  // staged now (streaming stores), compared with the leader's copy in the same pass
-            uint64_t off = 0;
-            if (efes::upload_stage_if_same(u, p, z->scratch, n, &off, &same) != EFES_OK) {
-              drop_pending(z);  // the fault is latched in the upload for the sync points
-              return EFES_OK;
-            }
-            if (same) drop_pending(z);
-          } else if (memcmp(pending(z), p, n) == 0) {
-            same = true;
-            z->open = false;
-          }
-          if (same) {
-            (void)efes::upload_confirm(u, sh);  // a fault is latched in the upload for the sync points
-            PairCounters& k = counters();
-            k.fused_writes.fetch_add(1, std::memory_order_relaxed);
-            k.fused_bytes.fetch_add(n, std::memory_order_relaxed);
-            return EFES_OK;
-          }
-        }
-      }
-    } else {  // the leader: stage, and wait for the follower's Write to match
-      if (n == 0) return EFES_OK;  // crc32.go:76-86 of nothing
-      if (!z->open && n <= efes::upload_chunk_bytes(u)) {
-        const PairStage m = pair_stage();
-        if (m == PairStage::kScratch) {
-          size_t cap = 0;
-          if (uint8_t* b = scratch_get(n, &cap)) {
-            memcpy(b, p, n);
-            z->scratch = b;
-            z->scratch_cap = cap;
-            z->open = true;
-            z->op = p;
-            z->on_bytes = n;
-            return EFES_OK;
-          }  // no memory for a scratch buffer: split
-        } else {
-          uint64_t off = 0;
-          if (efes::upload_stage(u, p, n, &off, m == PairStage::kCached) == EFES_OK) {
-            z->open = true;
-            z->op = p;
-            z->on_bytes = n;
-            z->ooff = off;
-          }  // else the fault is latched in the upload
-          return EFES_OK;
-        }
-      }
-    }
+  const uint8_t* p = static_cast<const uint8_t*>(p0);
+  size_t n = n0;
+  efes_sha1_state whole{};
+  bool split_mid = false;  // the rest of a Write the pair confirmed in part
+  if (c.z) {
+    if (d->sha() ? follow(c, p, n, &whole, &split_mid) : lead(c, p, n)) return EFES_OK;
     c.split();  // the Writes diverged: both continue alone
   }
   if (d->latched) return d->latched == EFES_ERR_STATE ? EFES_ERR_STATE : EFES_OK;
-  if (d->sha() && !d->u && n > 0 && fuse_enabled() && try_bind(d, p, n)) return EFES_OK;
+  if (!split_mid && n > 0 && !d->u && fuse_enabled()) {
+    if (d->sha()) {
+      const Bind b = try_bind(c, p, n);
+      if (b == Bind::kDone) return EFES_OK;
+      if (b == Bind::kPending) {
+        if (follow(c, p, n, &whole, &split_mid)) return EFES_OK;
+        c.split();
+        if (d->latched) return d->latched == EFES_ERR_STATE ? EFES_ERR_STATE : EFES_OK;
+      }
+    } else if (pair_stage() == PairStage::kScratch) {
+      // a CRC digest's first Write on a fresh upload waits for its MultiWriter partner
+      size_t cap = 0;
+      if (uint8_t* b = scratch_get(n, &cap)) {
+        memcpy(b, p, n);
+        d->defer = b;
+        d->defer_cap = cap;
+        d->defer_n = n;
+        candidate(d, p, n);
+        return EFES_OK;
+      }
+    }
+  }
   const bool fresh = !d->u;
   int rc = acquire(d);
   if (rc == EFES_OK) rc = efes_upload_write(d->u, p, n);
+  if (rc == EFES_OK && split_mid) efes::upload_set_shadow(d->u, whole);  // Go made ONE Write of it
   if (rc == EFES_OK) {
-    if (!d->sha() && fresh && n > 0 && fuse_enabled() && efes::upload_holds_only(d->u, n)) candidate(d, p, n);
+    if (!d->sha() && fresh && n > 0 && fuse_enabled() && pair_stage() != PairStage::kScratch &&
+        efes::upload_holds_only(d->u, n))
+      candidate(d, p, n);
     return EFES_OK;
   }
   d->latched = rc;
@@ -774,7 +911,7 @@ template <class D>
 void digest_free(D* d) {
   if (!d) return;
   {
-    Call c(d);
+    Call c(d, false);
     if (c.z) c.leave(false);
     drop(d);
   }
@@ -955,7 +1092,7 @@ void efes_crc32_free(efes_crc32* d) { digest_free(d); }
 
 void efes_crc32_reset(efes_crc32* d) {  // crc32.go:74
   if (!d) return;
-  Call c(d);
+  Call c(d, false);
   if (c.z) c.leave(false);
   drop(d);
   d->cbase.crc = 0;
@@ -995,7 +1132,7 @@ int efes_crc32_unmarshal_text(efes_crc32* d, const char* text, size_t n) {  // c
   efes_crc32_state s;
   const int rc = efes_crc32_state_unmarshal_text(&s, text, n);
   if (rc) return rc;
-  Call c(d);
+  Call c(d, false);
   if (c.z) c.leave(false);
   drop(d);
   d->cbase = s;

@@ -322,3 +322,39 @@ def test_diverging_pairs_other_staging_modes(gpu, mode):
     r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, EFES_PAIR_STAGE=mode),
                        capture_output=True, text=True, timeout=110)
     assert r.returncode == 0 and "ok" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])
+
+
+def test_large_writes_fuse_and_split_mid_write(gpu, oracle, oracle_lib):
+    """Writes larger than a staging chunk (256 KiB): the MultiWriter pattern still fuses completely
+    (the CRC Write waits in a scratch buffer, the SHA-1 Write stages it chunk by chunk); a buffer
+    changed between the two Writes past the first chunk splits the pair mid-Write, and the SHA-1
+    state is still Go's after ONE Write (MarshalText compares x with its stale bytes)."""
+    h = gpu["hashing"]
+    gpu = dict(gpu, oracle_lib=oracle_lib)
+    ctx = h.Context(0)
+    pool = h.Pool([ctx])
+    buf = _buf(3_000_000, 4242)
+    o = Obj(gpu, oracle, ctx)
+    s0 = _stats(gpu)
+    total = 0
+    for off, n in ((0, 1000), (1000, (1 << 20) + 37), (1000 + (1 << 20) + 37, 700_001)):  # odd sizes: pieces
+        o.crc_write(buf, off, n)                                                          # straddle blocks
+        o.sha_write(buf, off, n)
+        total += n
+    o.check_texts(True, "large fused")
+    d = _delta(s0, _stats(gpu))
+    assert d["pairs"] == 1 and d["settles"] == 0 and d["fused_bytes"] == total, d
+    assert pool.stats(0).bytes == total
+    for k, at in enumerate((600_000, 300, 699_999)):  # past the first pieces, in the first, in the last
+        off = 100_000 + 7 * k
+        o.crc_write(buf, off, 700_000)
+        buf[off + at] ^= 0x5A
+        o.sha_write(buf, off, 700_000)
+        o.check_texts(k % 2 == 0, f"split mid-Write at {at}")
+        o.crc_write(buf, off + 3, 333_333)  # and the pair forms again
+        o.sha_write(buf, off + 3, 333_333)
+    o.check_sums(True, "end")
+    assert _delta(s0, _stats(gpu))["settles"] >= 3
+    del o
+    pool.close()
+    ctx.close()

@@ -351,8 +351,8 @@ def test_large_writes_fuse_and_split_mid_write(gpu, oracle, oracle_lib):
         buf[off + at] ^= 0x5A
         o.sha_write(buf, off, 700_000)
         o.check_texts(k % 2 == 0, f"split mid-Write at {at}")
-        o.crc_write(buf, off + 3, 333_333)  # and the pair forms again
-        o.sha_write(buf, off + 3, 333_333)
+        o.crc_write(buf, off + 3, 333_333)  # alone (the SHA-1 digest holds an upload after the split);
+        o.sha_write(buf, off + 3, 333_333)  # the next check_texts parks both and the pair binds again
     o.check_sums(True, "end")
     assert _delta(s0, _stats(gpu))["settles"] >= 3
     del o

@@ -290,10 +290,11 @@ typedef struct efes_crc32 efes_crc32;
  * buffer to the CRC digest and then, unchanged, to the SHA-1 digest.  The library detects that
  * pattern and binds the two digests to ONE upload keeping both hashes, so each byte is staged once
  * and hashed by one fused job, as efes_upload_* does for a caller that asks for it:
- *   - a CRC digest's Write that opens a fresh upload is a candidate; a parked SHA-1 digest's Write
- *     with the same pointer and length binds to it when the staged bytes equal its own (memcmp);
- *   - then each CRC Write is staged but held back until the SHA-1 Write of the same (p, n), checked
- *     against the staged bytes, confirms it;
+ *   - a CRC digest's first Write after a sync point is held back (copied) as a candidate; a parked
+ *     SHA-1 digest's Write with the same pointer and length binds to it, and the pair opens one
+ *     upload (a candidate nobody binds is staged at the CRC digest's next call);
+ *   - then each CRC Write is held back until the SHA-1 Write of the same (p, n) -- of any size --
+ *     is staged and compared with it in one pass, which confirms it;
  *   - anything else (a Write to one digest only, other bytes, the CRC digest synced first, Reset /
  *     UnmarshalText / free of one, an eviction) splits the pair: every confirmed byte is in both
  *     states, an unconfirmed CRC Write in the CRC state only, and both go on alone.
@@ -303,7 +304,7 @@ typedef struct efes_crc32 efes_crc32;
  * Process-wide counters: */
 typedef struct efes_pair_stats {
     uint64_t pairs;         /* CRC + SHA-1 digests bound to one upload */
-    uint64_t fused_writes;  /* SHA-1 Writes served by the CRC Write's staged bytes (no copy, no job) */
+    uint64_t fused_writes;  /* SHA-1 Writes confirming the CRC Write (one staging copy, one job) */
     uint64_t fused_bytes;   /* their bytes */
     uint64_t settles;       /* pairs split (diverging Writes, evictions) */
 } efes_pair_stats;

@@ -1697,17 +1697,19 @@ hipError_t launch_fed(const efes_job* jobs, uint32_t njobs, const Tables* tabs, 
   return launch_fed_shape<kFed4G, kFed4C>(jobs, njobs, tabs, s);          // FED4
 }
 
+// EFES_WIDE_PACE=0 (A/B): read once, when the library is loaded.
+static const bool g_wide_pace_off = [] {
+  const char* e = getenv("EFES_WIDE_PACE");
+  return e && *e == '0';
+}();
+
 hipError_t launch_wide(const efes_job* jobs, uint32_t njobs, const Tables* tabs, hipStream_t s, bool exclusive,
                        int cus) {
   if (njobs == 0) return hipSuccess;
   // waves per SIMD of the launch: a workgroup per CU holds all of its SIMDs' waves (wide_pace);
   // exclusive parts (one wave per SIMD on reserved CUs) and EFES_WIDE_PACE=0 use 4-wave groups.
   const uint64_t waves = (njobs + 63) / 64, simds = 4ull * (uint64_t)(cus > 0 ? cus : 256);
-  static const bool pace_off = [] {
-    const char* e = getenv("EFES_WIDE_PACE");
-    return e && *e == '0';
-  }();
-  const uint32_t wps = exclusive || pace_off ? 1u : (uint32_t)std::min<uint64_t>(kWideMaxWps, (waves + simds - 1) / simds);
+  const uint32_t wps = exclusive || g_wide_pace_off ? 1u : (uint32_t)std::min<uint64_t>(kWideMaxWps, (waves + simds - 1) / simds);
   const uint32_t per = 64 * kWideWaves * wps;
   const size_t xs = (size_t)per * kXStride;  // the lanes' tail buffers (dynamic LDS)
   // The kernel's static LDS, and the dynamic-LDS limit raised once to the rest of the CU's LDS

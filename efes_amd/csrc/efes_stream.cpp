@@ -151,13 +151,6 @@ int64_t now_ns() {
 // waited this long itself it evicts the oldest idle holder, active or not (progress).  Evicting
 // active holders at once made every Write of an over-subscribed queue settle another upload and
 // wait for the GPU (EFES_DIGEST_EVICT_MS=0 restores that).
-int64_t evict_patience_ns() {
-  static const int64_t ns = [] {
-    const char* e = getenv("EFES_DIGEST_EVICT_MS");
-    return (e && *e ? strtoll(e, nullptr, 10) : 50) * 1000000ll;
-  }();
-  return ns;
-}
 
 // Where the leader's Write waits for the follower's (EFES_PAIR_STAGE):
 //   scratch -- (default) copied into a cache-hot per-thread scratch buffer; the follower's Write
@@ -169,15 +162,28 @@ int64_t evict_patience_ns() {
 // stream 46.3-47.5 GiB/s, efes_upload 48.9-49.3; on another (r04_pair_stage_ab) stream ran 35.2-39.8
 // against cached 43.5-43.7.
 enum class PairStage { kCached, kStream, kScratch };
-PairStage pair_stage() {
-  static const PairStage m = [] {
-    const char* e = getenv("EFES_PAIR_STAGE");
-    if (e && !strcmp(e, "stream")) return PairStage::kStream;
-    if (e && !strcmp(e, "cached")) return PairStage::kCached;
-    return PairStage::kScratch;
-  }();
-  return m;
-}
+
+// The environment switches above, read once when the library is loaded (by one thread, before any
+// call): function-local statics initialised on first use are first read by request threads racing
+// each other.
+struct Env {
+  int64_t evict_patience_ns = 50 * 1000000ll;
+  bool fuse = true;
+  PairStage stage = PairStage::kScratch;
+  Env() {
+    if (const char* e = getenv("EFES_DIGEST_EVICT_MS"); e && *e) evict_patience_ns = strtoll(e, nullptr, 10) * 1000000ll;
+    if (const char* e = getenv("EFES_DIGEST_FUSE"); e && !strcmp(e, "0")) fuse = false;
+    if (const char* e = getenv("EFES_PAIR_STAGE")) {
+      if (!strcmp(e, "stream")) stage = PairStage::kStream;
+      if (!strcmp(e, "cached")) stage = PairStage::kCached;
+    }
+  }
+};
+const Env g_env;
+
+int64_t evict_patience_ns() { return g_env.evict_patience_ns; }
+bool fuse_enabled() { return g_env.fuse; }
+PairStage pair_stage() { return g_env.stage; }
 
 // Scratch buffers for PairStage::kScratch: a few per thread, reused last-in first-out so the one a
 // leader Write copies into is still in this core's cache when the follower's Write (normally on
@@ -232,13 +238,6 @@ void scratch_put(uint8_t* p, size_t cap) {
   t_scratch[t_nscratch++] = ScratchBuf{p, cap};
 }
 
-bool fuse_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("EFES_DIGEST_FUSE");
-    return !(e && !strcmp(e, "0"));
-  }();
-  return on;
-}
 
 bool reclaim_chunks(void* arg);
 

@@ -5,9 +5,14 @@ set -uo pipefail
 cd "${GRAFT_REPO_ROOT:?}" || exit 1
 O=gpurun_out/${1:-r04_ingest_ab}
 mkdir -p "$O"
-for rep in 1 2; do
+for rep in ${REPS:-1 2}; do
+  if [ "${NEW_FIRST:-0}" = 1 ]; then
+    timeout -k 10 300 python3 bench.py --workload ingest --no-cpu-baseline > "$O/new.$rep.json" 2> "$O/new.$rep.err" || exit 1
+  fi
   timeout -k 10 300 env EFES_LIB_OVERRIDE=$PWD/ab_old/libefeshash.so python3 bench.py --workload ingest --no-cpu-baseline > "$O/old.$rep.json" 2> "$O/old.$rep.err" || exit 1
-  timeout -k 10 300 python3 bench.py --workload ingest --no-cpu-baseline > "$O/new.$rep.json" 2> "$O/new.$rep.err" || exit 1
+  if [ "${NEW_FIRST:-0}" != 1 ]; then
+    timeout -k 10 300 python3 bench.py --workload ingest --no-cpu-baseline > "$O/new.$rep.json" 2> "$O/new.$rep.err" || exit 1
+  fi
   python3 - "$O" $rep <<'PY' | tee -a "$O/ab.log"
 import json, sys
 O, r = sys.argv[1:3]

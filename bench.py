@@ -95,7 +95,8 @@ def parse_args(argv=None):
                         "flight, 8192 x 4 MiB, 32 KiB pageable Writes, Sum each); auto = N=1 only")
     p.add_argument("--go-surface-leg", choices=["auto", "on", "off"], default="auto",
                    help="also report the UNCHANGED Go surface (tools/bench_go_surface: hash_gpu.go's calls under "
-                        "saveFile, fused MultiWriter pairs and EFES_DIGEST_FUSE=0) at uploads_path's concurrency "
+                        "saveFile, fused MultiWriter pairs, and the SHA-1 Writes from a copy: never fused) at "
+                        "uploads_path's concurrency "
                         "(auto: N=1)")
     p.add_argument("--latency-leg", choices=["auto", "on", "off"], default="auto",
                    help="also report per-PATCH latency at 1/16/256 uploads in flight, GPU vs the CPU port (auto: N=1)")
@@ -261,8 +262,9 @@ def go_surface_leg(uploads=None):
     uploads_path's concurrency (32 request threads x 256 uploads in flight, 8 192 x 4 MiB, 32 KiB
     io.Copy buffers): per PATCH efes_sha1_new_pool + efes_crc32_new_pool, efes_crc32_write then
     efes_sha1_write of the SAME buffer (MultiWriter(f, CRC32, Sha1), filereceiver.go:208-209), Sum of
-    both.  The library fuses each pair into one upload (efes_stream.cpp); the same run with
-    EFES_DIGEST_FUSE=0 (two uploads, each byte staged and hashed twice) is reported beside it.
+    both.  The library fuses each pair into one upload (efes_stream.cpp); the same run with the SHA-1
+    digest written from an equal copy of each buffer (the pair never binds: two uploads, each byte
+    staged and hashed twice, round 3's behaviour) is reported beside it.
     Digests checked against hashlib/zlib.  Returns the result dict (not the metric)."""
     import hashlib
     import subprocess
@@ -271,19 +273,19 @@ def go_surface_leg(uploads=None):
     exe = os.path.join(ROOT, "tools", "bench_go_surface")
     cmd = [exe, "32", "8192", str(4 << 20), str(32 << 10), "256", "1", "256", "8208"]
 
-    def run(fuse):
-        r = subprocess.run(cmd, check=True, capture_output=True, text=True, timeout=300,
-                           env=dict(os.environ, EFES_DIGEST_FUSE=fuse))
+    def run(writes):
+        r = subprocess.run(cmd + ["-", writes], check=True, capture_output=True, text=True, timeout=300)
         return json.loads(r.stdout.strip().splitlines()[-1])
 
     src = _xorshift_bytes(4 << 20)
     want = hashlib.sha1(src).hexdigest() + "%08x" % zlib.crc32(src)
-    res = run("1")
+    res = run("same")
     res["digests_match"] = res.pop("sum_sha1_crc32") == want and res.pop("all_equal")
-    un = run("0")
+    un = run("copy")
     res["unfused"] = {"value": un["value"], "unit": "GiB/s", "hashed_bytes_per_byte": un["hashed_bytes_per_byte"],
                       "launches": un["launches"], "digests_match": un["sum_sha1_crc32"] == want and un["all_equal"],
-                      "note": "EFES_DIGEST_FUSE=0: the CRC and SHA-1 digests as two uploads"}
+                      "note": "SHA-1 Writes from an equal copy of each buffer: the CRC and SHA-1 digests as two "
+                              "uploads"}
     if uploads and uploads.get("value"):
         res["vs_uploads_path"] = round(res["value"] / uploads["value"], 4)
     res["note"] = ("unchanged Go call sequence (hash_gpu.go): pooled NewSha1 + NewCRC32IEEE per PATCH, 32 KiB "
@@ -469,7 +471,7 @@ def make_workload(args, rank: int, world: int, ctx, device: str, stream):
     import torch
 
     from efes_amd.batch import DeviceBatch
-    from efes_amd.chunksize import MIXED_CLASSES
+    from efes_amd.chunksize import mixed_geometry
 
     kw = dict(sha1=True, crc32=not args.sha1_only, finalize=True, fresh=True, ctx=ctx, device=device)
     seed = 0xEFE5 ^ (rank << 32)
@@ -489,10 +491,7 @@ def make_workload(args, rank: int, world: int, ctx, device: str, stream):
     data = torch.empty(pool, dtype=torch.uint8, device=device)
     ctx.fill_synthetic(data.data_ptr(), pool, seed, stream.cuda_stream)
     if args.workload == "mixed":
-        rng = np.random.default_rng(7 + rank)
-        sizes = np.asarray(MIXED_CLASSES, dtype=np.uint64)[rng.integers(0, len(MIXED_CLASSES), args.mixed_chunks)]
-        sizes = np.sort(sizes)[::-1].copy()  # longest first: equal lengths per wave, LPT tail
-        offs = (rng.integers(0, (pool - sizes.astype(np.int64)) // 256 + 1) * 256).astype(np.uint64)
+        sizes, offs = mixed_geometry(args.mixed_chunks, pool, 7 + rank)  # longest first
         L = max(1, args.mixed_launches)
         batches = [DeviceBatch(data.data_ptr(), offs[k::L], sizes[k::L], **kw) for k in range(L)]
         total = int(sizes.sum())
@@ -554,7 +553,113 @@ N_SIMD = 1024
 VALU_CYC = 4
 
 
-def binding_roofline(kernel: str, achieved_gbs: float, concurrent_msgs: int, sha1_only: bool):
+class ClockMeter:
+    """The effective engine clock over a timed region (the VALU-issue ceilings scale with it), read two
+    ways at once:
+      probe -- two marker launches on the measured stream (tools/clockprobe.hip) bracket the region;
+               each records s_memtime (shader clock, per XCD) and s_memrealtime (100 MHz) per XCD;
+      smi   -- amdsmi's per-XCD current_gfxclk, polled every 2 ms by a host thread, averaged.
+    Calibrated against GRBM_GUI_ACTIVE / 8 / ns of the same kernels (profiles/r05_clock/).  Either
+    may be missing (no probe library, no amdsmi): the leg then reports what it has."""
+
+    def __init__(self, dev_index: int):
+        import ctypes
+
+        self.dev = dev_index
+        self.probe = None
+        self.smi = None
+        path = os.path.join(ROOT, "tools", "libclockprobe.so")
+        bdf = None
+        if os.path.exists(path):
+            try:
+                self.probe = ctypes.CDLL(path)
+                self.probe.clockprobe_mark.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+                self.probe.clockprobe_read.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+                                                       ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]
+                buf = ctypes.create_string_buffer(64)
+                if self.probe.clockprobe_pci_bus_id(dev_index, buf, 64) == 0:
+                    bdf = buf.value.decode().lower()
+            except (OSError, AttributeError):
+                self.probe = None
+        try:
+            import amdsmi
+
+            amdsmi.amdsmi_init()
+            handles = amdsmi.amdsmi_get_processor_handles()
+            pick = handles[dev_index] if dev_index < len(handles) else None
+            for h in handles:
+                if bdf and str(amdsmi.amdsmi_get_gpu_device_bdf(h)).lower() == bdf:
+                    pick = h
+            if pick is not None:
+                amdsmi.amdsmi_get_gpu_metrics_info(pick)
+                self.smi = (amdsmi, pick)
+        except Exception:  # noqa: BLE001 -- amdsmi absent or refused: the probe alone
+            self.smi = None
+        self._thread = None
+        self._samples = []
+        self._stop = False
+        self._marked = False
+
+    def _poll(self):
+        amdsmi, h = self.smi
+        while not self._stop:
+            try:
+                m = amdsmi.amdsmi_get_gpu_metrics_info(h)
+                v = [float(x) for x in m.get("current_gfxclks", []) if isinstance(x, (int, float)) and 0 < x < 65535]
+                if v:
+                    self._samples.append(sum(v) / len(v))
+            except Exception:  # noqa: BLE001
+                return
+            time.sleep(0.002)
+
+    def start(self, stream: int):
+        """Before the region's first launch on `stream` (a hipStream_t handle)."""
+        import threading
+
+        self._samples, self._stop = [], False
+        self._marked = self.probe is not None and self.probe.clockprobe_mark(self.dev, stream, 0) == 0
+        if self.smi:
+            self._thread = threading.Thread(target=self._poll, daemon=True)
+            self._thread.start()
+
+    def end(self, stream: int):
+        """After the region's last launch on `stream`, before the caller synchronizes."""
+        if self._marked:
+            self._marked = self.probe.clockprobe_mark(self.dev, stream, 1) == 0
+
+    def stop(self) -> dict:
+        """After the caller synchronized the stream."""
+        import ctypes
+
+        out = {"unit": "MHz"}
+        if self._marked:
+            mhz, sec, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_int()
+            if self.probe.clockprobe_read(self.dev, ctypes.byref(mhz), ctypes.byref(sec), ctypes.byref(n)) == 0:
+                out.update({"probe_mhz": round(mhz.value, 1), "probe_seconds": round(sec.value, 4),
+                            "probe_xcds": n.value})
+        if self._thread:
+            self._stop = True
+            self._thread.join()
+            self._thread = None
+            if self._samples:
+                s = sorted(self._samples)
+                out.update({"smi_mhz_mean": round(sum(s) / len(s), 1), "smi_mhz_min": round(s[0], 1),
+                            "smi_mhz_max": round(s[-1], 1), "smi_samples": len(s)})
+        out["mhz"] = out.get("smi_mhz_mean", out.get("probe_mhz"))
+        return out
+
+
+_CLOCK = None
+
+
+def clock_meter(dev_index: int):
+    global _CLOCK
+    if _CLOCK is None or _CLOCK.dev != dev_index:
+        _CLOCK = ClockMeter(dev_index)
+    return _CLOCK
+
+
+def binding_roofline(kernel: str, achieved_gbs: float, concurrent_msgs: int, sha1_only: bool, clock=None):
     if kernel == "deep_kernel":
         ceiling = min(concurrent_msgs, N_SIMD) * 64 * CLOCK_HZ / (405 * VALU_CYC) / 1e9
         model = ("serial SHA-1 chain: each of min(messages, 1024 SIMDs) messages advances one 64-B block per "
@@ -565,14 +670,19 @@ def binding_roofline(kernel: str, achieved_gbs: float, concurrent_msgs: int, sha
         ceiling = min(lanes / 64, N_SIMD) * 64 * 64 * CLOCK_HZ / (per_block * VALU_CYC) / 1e9
         model = (f"VALU issue: {per_block} VALU per 64-B block per wave of 64 messages, 4 cycles each, "
                  "every SIMD busy at 2.4 GHz")
-    return {"bound": "valu-issue", "achieved": round(achieved_gbs, 2), "ceiling": round(ceiling, 2), "unit": "GB/s",
-            "frac": round(achieved_gbs / ceiling, 4), "model": model}
+    out = {"bound": "valu-issue", "achieved": round(achieved_gbs, 2), "ceiling": round(ceiling, 2), "unit": "GB/s",
+           "frac": round(achieved_gbs / ceiling, 4), "model": model}
+    mhz = (clock or {}).get("mhz")
+    if mhz:  # the same ceiling at the clock the region actually ran at
+        at = ceiling * mhz * 1e6 / CLOCK_HZ
+        out.update({"clock_mhz": mhz, "ceiling_at_clock": round(at, 2), "frac_at_clock": round(achieved_gbs / at, 4)})
+    return out
 
 
 def run_timed(batches, steps: int, warmup: int, mode: int, device: str, stream, dist, progress: bool = False):
     """W untimed warm-up launches, then exactly `steps` launches bracketed by barrier +
     synchronize; returns (wall seconds of this rank, average kernel ms from HIP events recorded
-    on the launch stream)."""
+    on the launch stream, the effective engine clock over the timed launches (ClockMeter))."""
     import torch
 
     for _ in range(warmup):
@@ -584,6 +694,8 @@ def run_timed(batches, steps: int, warmup: int, mode: int, device: str, stream, 
     if dist:
         dist.barrier()
     torch.cuda.synchronize(device)
+    clk = clock_meter(torch.device(device).index or 0)
+    clk.start(stream.cuda_stream)
     t0 = time.perf_counter()
     ev0.record(stream)
     for k in range(steps):
@@ -593,13 +705,15 @@ def run_timed(batches, steps: int, warmup: int, mode: int, device: str, stream, 
             print(f"[bench] step {k + 1}/{steps} done at {time.perf_counter() - t0:.1f} s", file=sys.stderr,
                   flush=True)
     ev1.record(stream)
+    clk.end(stream.cuda_stream)
     torch.cuda.synchronize(device)
     if dist:
         dist.barrier()
     wall = time.perf_counter() - t0
+    clock = clk.stop()
     for b in batches:
         assert (b.status_host() == 0).all(), "hash jobs reported an error status"
-    return wall, ev0.elapsed_time(ev1) / max(1, steps)
+    return wall, ev0.elapsed_time(ev1) / max(1, steps), clock
 
 
 def ingest_leg(args, rank: int, world: int, ctx, device: str, stream, mode: int, dist=None):
@@ -619,7 +733,7 @@ def ingest_leg(args, rank: int, world: int, ctx, device: str, stream, mode: int,
     a.workload, a.ingest_batch, a.ingest_scale = "ingest", 196608, args.ingest_scale
     with torch.cuda.stream(stream):
         data, batches, step_bytes, config = make_workload(a, rank, world, ctx, device, stream)
-        wall, kernel_ms = run_timed(batches, len(batches), 1, mode, device, stream, dist)
+        wall, kernel_ms, clock = run_timed(batches, len(batches), 1, mode, device, stream, dist)
         ok = ingest_spot_check(data, batches, config)
     from efes_amd.shard import max_over_ranks
 
@@ -644,7 +758,8 @@ def ingest_leg(args, rank: int, world: int, ctx, device: str, stream, mode: int,
                          "traffic": None if ratio is None else round(ratio * per_launch),
                          "traffic_per_algorithmic_byte": None if ratio is None else round(ratio, 4),
                          "algorithmic_bytes_per_launch": int(per_launch)},
-            "binding_roofline": binding_roofline("wide_kernel", achieved, per_launch_jobs, args.sha1_only),
+            "binding_roofline": binding_roofline("wide_kernel", achieved, per_launch_jobs, args.sha1_only, clock),
+            "clock": clock,
             "note": "many concurrent chunks per GPU (configs[4] per-GPU queue); value = all ranks' bytes / the "
                     "slowest rank's wall time; roofline = this rank's kernel; not the headline `value`"}
 
@@ -664,7 +779,7 @@ def sha1_only_leg(args, ctx, data, fused, device: str, stream):
     with torch.cuda.stream(stream):
         b = DeviceBatch(data.data_ptr(), np.arange(n, dtype=np.uint64) * chunk, np.full(n, chunk), crc32=False,
                         fresh=True, ctx=ctx, device=device)
-        wall, kernel_ms = run_timed([b], args.steps, 1, MODE_AUTO, device, stream, None)
+        wall, kernel_ms, clock = run_timed([b], args.steps, 1, MODE_AUTO, device, stream, None)
     kernel = kernel_names()[lib().efes_auto_mode(ctx.handle, n)]
     achieved = n * chunk / (kernel_ms * 1e-3) / 1e9
     ok = b.sha1_hex() == fused.sha1_hex() and bool((b.sums_host()[:, 20:] == 0).all())
@@ -674,8 +789,8 @@ def sha1_only_leg(args, ctx, data, fused, device: str, stream):
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 5), "kernel_ms": round(kernel_ms, 4),
                          "traffic": load_traffic(kernel, f"{n}x{chunk}:sha1")},
-            "binding_roofline": binding_roofline(kernel, achieved, n, True) if kernel in ("deep_kernel", "wide_kernel")
-            else None,
+            "binding_roofline": binding_roofline(kernel, achieved, n, True, clock)
+            if kernel in ("deep_kernel", "wide_kernel") else None, "clock": clock,
             "digests_match_fused_sha1": ok, "note": "same chunks as the metric, SHA-1 only; not `value`"}
 
 
@@ -729,10 +844,10 @@ def concurrency_leg(args, ctx, device: str, stream):
             else:
                 base = DeviceBatch(data.data_ptr(), offs, np.full(n, seg), ctx=ctx, device=device)
                 batches = [base.variant(fresh=k == 0, finalize=k == 3) for k in range(4)]
-            wall, kernel_ms = run_timed(batches, 2 * len(batches), 1, MODE_AUTO, device, stream, None)
+            wall, kernel_ms, clock = run_timed(batches, 2 * len(batches), 1, MODE_AUTO, device, stream, None)
             points.append({"chunks": n, "kernel": names[lib().efes_auto_mode(ctx.handle, n)],
                            "segments": len(batches), "GiB/s": round(2 * n * chunk / wall / GiB, 1),
-                           "ms_per_launch": round(kernel_ms, 2)})
+                           "ms_per_launch": round(kernel_ms, 2), "clock_mhz": clock.get("mhz")})
             del batches, data
             torch.cuda.empty_cache()
     return {"unit": "GiB/s", "chunk_bytes": chunk, "points": points,
@@ -760,7 +875,7 @@ def mixed_leg(args, rank: int, world: int, ctx, device: str, stream):
         data, batches, step_bytes, config = make_workload(a, rank, world, ctx, device, stream)
         for b in batches:
             b.make_plan()
-        wall, kernel_ms = run_timed(batches, len(batches), 1, MODE_PLAN, device, stream, None)
+        wall, kernel_ms, clock = run_timed(batches, len(batches), 1, MODE_PLAN, device, stream, None)
     total = sum(step_bytes)
     names = kernel_names()
     parts = [{"jobs": j, "kernel": names[m], "exclusive_cus": x} for j, m, x in batches[0].plan.parts()]
@@ -771,7 +886,7 @@ def mixed_leg(args, rank: int, world: int, ctx, device: str, stream):
             "chunks": config["chunks_per_gpu"], "bytes": total, "plan": parts,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 5), "kernel_ms": round(kernel_ms, 3)},
-            "note": "makespan set by the 64 MiB chunks' SHA-1 chains (DESIGN.md §4 batch planner); not `value`"}
+            "clock": clock, "note": "makespan set by the 64 MiB chunks' SHA-1 chains (DESIGN.md §4 batch planner); not `value`"}
 
 
 def span_crc_leg(args, ctx, device: str, stream, gib: int = 16, reps: int = 5):
@@ -792,12 +907,16 @@ def span_crc_leg(args, ctx, device: str, stream, gib: int = 16, reps: int = 5):
         ctx.crc32_span(data.data_ptr(), n, st.data_ptr(), stream.cuda_stream)  # warm-up
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         stream.synchronize()
+        clk = clock_meter(torch.device(device).index or 0)
+        clk.start(stream.cuda_stream)
         e0.record(stream)
         for _ in range(reps):
             st.zero_()
             ctx.crc32_span(data.data_ptr(), n, st.data_ptr(), stream.cuda_stream)
         e1.record(stream)
+        clk.end(stream.cuda_stream)
         stream.synchronize()
+        clock = clk.stop()
         ms = e0.elapsed_time(e1) / reps
         st.zero_()
         ctx.crc32_span(data.data_ptr(), 1 << 30, st.data_ptr(), stream.cuda_stream)
@@ -818,7 +937,7 @@ def span_crc_leg(args, ctx, device: str, stream, gib: int = 16, reps: int = 5):
                          "frac": round(achieved / HBM_PEAK_GBPS, 4), "ms_per_call": round(ms, 3)},
             "cpu_port_1core": {"value": round((1 << 30) / cpu_s / GiB, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
                                "sample": "oracle crc32digest.Write (slicing-by-8, crc32.go:153-169) over the first GiB"},
-            "crc_matches_zlib": ok, "note": "HIP events on the launch stream; not `value`"}
+            "crc_matches_zlib": ok, "clock": clock, "note": "HIP events on the launch stream; not `value`"}
 
 
 def main(argv=None):
@@ -867,7 +986,7 @@ def main(argv=None):
             for b in batches:
                 b.make_plan()  # host-side planning stays outside the timed region
         steps = args.steps if len(batches) == 1 else len(batches)
-        wall, kernel_ms = run_timed(batches, steps, args.warmup, mode, device, stream, dist, args.progress)
+        wall, kernel_ms, clock = run_timed(batches, steps, args.warmup, mode, device, stream, dist, args.progress)
     wall = max_over_ranks(wall, device if args.dist_backend == "nccl" else None)  # slowest rank
 
     bytes_timed = sum(step_bytes[k % len(step_bytes)] for k in range(steps))
@@ -912,8 +1031,9 @@ def main(argv=None):
             "kernel_ms": round(kernel_ms, 4),
             "algorithmic_bytes_per_launch": int(per_launch),
         },
-        "binding_roofline": (binding_roofline(kernel_name, achieved, njobs, args.sha1_only)
+        "binding_roofline": (binding_roofline(kernel_name, achieved, njobs, args.sha1_only, clock)
                              if kernel_name in ("deep_kernel", "wide_kernel") else None),
+        "clock": clock,
         "cpu_baseline": None,
     }
     if plan:

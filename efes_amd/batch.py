@@ -9,10 +9,40 @@ from __future__ import annotations
 
 import numpy as np
 
-from ._lib import EFES_JOB_FINALIZE, EFES_JOB_INIT, EFES_JOB_SUM_ONLY, JOB_DTYPE, MODE_AUTO, SHA1_STATE_DTYPE
+from ._lib import (EFES_JOB_FINALIZE, EFES_JOB_INIT, EFES_JOB_SUM_ONLY, JOB_DTYPE, MODE_AUTO, MODE_DEEP, MODE_FED4,
+                   MODE_FED4E, MODE_GROUP, MODE_WIDE, PLAN_MAX_PARTS, SHA1_STATE_DTYPE, Plan, PlanPart)
 from .hashing import Context, default_context
 
 MODE_PLAN = -1  # run(): efes_plan_batch + efes_hash_submit_plan instead of one fixed kernel shape
+
+# lanes per job -> kernel shape, in forced_plan's spec (64 = DEEP, 0 = WIDE, 1 = FED4, 2 = FED4E)
+_SPEC_MODES = {64: MODE_DEEP, 0: MODE_WIDE, 1: MODE_FED4, 2: MODE_FED4E, **MODE_GROUP}
+
+
+def forced_plan(n: int, spec: str) -> Plan:
+    """A caller-built efes_plan (efes_hash.h lets a caller place its own parts) for n longest-first
+    jobs: "<lanes>:<jobs>[x],..." -- lanes 64 = DEEP, 0 = WIDE, 1 = FED4, 2 = FED4E (both always own
+    their CUs), 4/8/16/32 = GROUPn; x = exclusive (CUs of its own) -- in order, the jobs beyond the
+    listed parts WIDE.  Raises ValueError for an unknown shape or more than PLAN_MAX_PARTS parts."""
+    parts, used = [], 0
+    for item in filter(None, spec.split(",")):
+        lanes, _, jobs = item.partition(":")
+        excl = jobs.endswith("x")
+        if int(lanes) not in _SPEC_MODES:
+            raise ValueError(f"unknown shape {lanes!r}")
+        take = min(int(jobs.rstrip("x")), n - used)
+        if take:
+            parts.append((take, _SPEC_MODES[int(lanes)], excl))
+        used += take
+    if used < n:
+        parts.append((n - used, MODE_WIDE, False))
+    if len(parts) > PLAN_MAX_PARTS:
+        raise ValueError(f"{len(parts)} parts > {PLAN_MAX_PARTS}")
+    plan = Plan()
+    plan.njobs, plan.nparts = n, len(parts)
+    for i, (j, m, x) in enumerate(parts):
+        plan.part[i] = PlanPart(j, m, 1 if x else 0, 0)
+    return plan
 
 IV = np.array([0x67452301, 0xEFCDAB89, 0x98BADCFE, 0x10325476, 0xC3D2E1F0], dtype=np.uint32)
 
@@ -128,9 +158,12 @@ class DeviceBatch:
         self.submit(mode)
         self.torch.cuda.synchronize(self.device)
 
-    def make_plan(self) -> None:
-        """efes_plan_batch over the job lengths; keeps a longest-first copy of the job array."""
+    def make_plan(self, force: str | None = None) -> None:
+        """efes_plan_batch over the job lengths; keeps a longest-first copy of the job array.  `force`
+        replaces the planner's parts by caller-built ones (forced_plan) over the same order."""
         order, self.plan = self.ctx.plan(self.jobs_host["length"])
+        if force is not None:
+            self.plan = forced_plan(self.n, force)
         self.jobs_planned = self.torch.from_numpy(self.jobs_host[order].view(np.uint8).copy()).to(self.device)
         self.torch.cuda.synchronize(self.device)
 

@@ -15,6 +15,7 @@ LIB_DIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIB_DIR, "libefeshash.so")
 SOURCES = ["efes_kernels.hip", "efes_crc_span.hip", "efes_api.cpp", "efes_ingest.cpp", "efes_queue.cpp", "efes_stream.cpp", "efes_plan.cpp"]
 HEADERS = ["efes_internal.hpp", "sha1_device.hpp"]
+PUBLIC_HEADERS = ["efes_hash.h", "efes_testing.h"]
 ARCH = "gfx950"
 
 
@@ -34,7 +35,7 @@ def _stale(target: str, deps: list[str]) -> bool:
 
 def build_lib(force: bool = False, verbose: bool = False) -> str:
     srcs = [os.path.join(CSRC, s) for s in SOURCES]
-    deps = srcs + [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(ROOT, "include", "efes_hash.h")]
+    deps = srcs + [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(ROOT, "include", h) for h in PUBLIC_HEADERS]
     if not force and not _stale(LIB, deps):
         return LIB
     os.makedirs(LIB_DIR, exist_ok=True)
@@ -77,6 +78,14 @@ def build_tools() -> list[str]:
                         src, "-o", exe, "-L", LIB_DIR, "-lefeshash", "-Wl,-rpath,$ORIGIN/../efes_amd/lib"], check=True)
     if os.path.exists(exe):
         out.append(exe)
+    src = os.path.join(ROOT, "tools", "clockprobe.hip")  # bench.py's engine-clock probe
+    so = os.path.join(ROOT, "tools", "libclockprobe.so")
+    if os.path.exists(src) and _stale(so, [src]):
+        subprocess.run([hipcc(), f"--offload-arch={ARCH}", "-O2", "-std=c++17", "-fPIC", "-shared", src, "-o", so + ".tmp"],
+                       check=True)
+        os.replace(so + ".tmp", so)
+    if os.path.exists(so):
+        out.append(so)
     src = os.path.join(ROOT, "tools", "bench_receiver.cpp")
     exe = os.path.join(ROOT, "tools", "bench_receiver")
     if os.path.exists(src) and _stale(exe, [src, RECEIVER_LIB, RECEIVER_HDR, LIB]):
@@ -132,6 +141,18 @@ def build_consumer_test() -> str:
     return exe
 
 
+def build_lifecycle_test() -> str:
+    """tests/c/efes_lifecycle_test_asan: the Go binding's object lifecycle against an AddressSanitizer
+    build of the library's host code (tools/asan_build.sh; test infrastructure)."""
+    exe = os.path.join(ROOT, "tests", "c", "efes_lifecycle_test_asan")
+    srcs = [os.path.join(CSRC, s) for s in SOURCES] + [os.path.join(CSRC, h) for h in HEADERS]
+    deps = srcs + [os.path.join(ROOT, "tests", "c", "efes_lifecycle_test.c"), os.path.join(ROOT, "tools", "asan_build.sh"),
+                   os.path.join(ROOT, "oracle", "liboracle.so")] + [os.path.join(ROOT, "include", h) for h in PUBLIC_HEADERS]
+    if _stale(exe, deps):
+        subprocess.run(["bash", os.path.join(ROOT, "tools", "asan_build.sh")], check=True)
+    return exe
+
+
 def build_oracle() -> str:
     """The CPU checker (test infrastructure; never linked into the product)."""
     subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
@@ -148,3 +169,4 @@ if __name__ == "__main__":
     print(build_consumer_test())
     print(build_receiver())
     print(build_receiver_test())
+    print(build_lifecycle_test())

@@ -63,3 +63,18 @@ def _go_mod(a: int, b: int) -> int:
 
 # The eleven ChunkSize values of the mixed benchmark (64K .. 64M).
 MIXED_CLASSES = [parse(f"{64 << k}K") if k < 4 else parse(f"{1 << (k - 4)}M") for k in range(11)]
+
+
+def mixed_geometry(n: int, pool_bytes: int, seed: int = 7):
+    """BASELINE configs[3]'s batch: n chunk sizes drawn uniformly from MIXED_CLASSES, longest first
+    (equal lengths per WIDE wave, LPT tail), each at a seeded 256-B aligned offset of a pool of
+    `pool_bytes` (chunks alias the pool: 752 GiB of chunks over 200 GiB at n = 65 536).  One function
+    for bench.py's mixed leg and its full-size parity test, so both hash the same geometry.
+    Returns (sizes, offsets) as uint64 arrays."""
+    import numpy as np
+
+    rng = np.random.default_rng(seed)
+    sizes = np.asarray(MIXED_CLASSES, dtype=np.uint64)[rng.integers(0, len(MIXED_CLASSES), n)]
+    sizes = np.sort(sizes)[::-1].copy()
+    offs = (rng.integers(0, (pool_bytes - sizes.astype(np.int64)) // 256 + 1) * 256).astype(np.uint64)
+    return sizes, offs

@@ -137,15 +137,8 @@ void efes::build_pos_tables(const Tables* t, PosTables* out) {
     }
 }
 
-// EFES_PART_STREAMS=plain: planned parts on plain streams (read once, when the library is loaded).
-static const bool g_plain_part_streams = [] {
-  const char* e = getenv("EFES_PART_STREAMS");
-  return e && !strcmp(e, "plain");
-}();
-
 // A stream on a hardware queue of its own (efes_internal.hpp).
 hipError_t efes::own_queue_stream(const efes_ctx* ctx, hipStream_t* out) {
-  if (g_plain_part_streams) return hipStreamCreateWithFlags(out, hipStreamNonBlocking);
   uint32_t all_cus[8];
   for (int w = 0; w < 8; ++w) {
     const int left = ctx->cus - 32 * w;

@@ -106,21 +106,14 @@ struct SpanLDS {
 };
 
 constexpr int kLineWords = kSpanLine / 4;
-#ifndef EFES_SPAN_BUF
-#define EFES_SPAN_BUF 2
-#endif
-constexpr int kSpanBuf = EFES_SPAN_BUF;  // lines in flight per lane
+constexpr int kSpanBuf = 2;  // lines in flight per lane (round 2 A/B, profiles/r02_span/)
 
 __device__ __forceinline__ void load_line(const uint8_t* src, uint32_t (&w)[kLineWords]) {
   typedef uint32_t v4u __attribute__((ext_vector_type(4)));
   const __attribute__((address_space(1))) v4u* s = (const __attribute__((address_space(1))) v4u*)src;
 #pragma unroll
   for (int q = 0; q < kLineWords / 4; ++q) {
-#ifdef EFES_SPAN_NT
-    const v4u v = __builtin_nontemporal_load(s + q);  // A/B knob: read once, nt policy
-#else
-    const v4u v = s[q];
-#endif
+    const v4u v = s[q];  // (a nontemporal load measured no faster, round 2)
     w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
   }
 }
@@ -248,10 +241,6 @@ hipError_t launch_crc_span(const void* data, uint64_t length, uint32_t* crc, con
   const uint64_t per_cu = kSpanWavesPerSimd / 4, resident = (uint64_t)(cus > 0 ? cus : 256) * per_cu;
   const uint64_t cap = resident < kSpanMaxGroups ? resident : (uint64_t)kSpanMaxGroups;
   if (groups > cap) groups = cap;
-  if (const char* e = getenv("EFES_SPAN_GROUPS")) {  // developer override for calibration
-    const uint64_t g = strtoull(e, nullptr, 10);
-    if (g >= 1 && g <= kSpanMaxGroups) groups = g;
-  }
   if (groups > nline) groups = nline;
   if (groups == 0) groups = 1;
   SpanArgs a{};

@@ -8,6 +8,7 @@
 #include <mutex>
 
 #include "../../include/efes_hash.h"
+#include "../../include/efes_testing.h"
 
 namespace efes {
 
@@ -58,29 +59,20 @@ void queue_set_fault_after(efes_queue* q, uint64_t k);
 // no lock held -- which hands over what it can (upload_handover) and returns whether it did.  The
 // digest queue (efes_stream.cpp).
 int queue_create_reclaiming(efes_ctx* ctx, uint64_t chunk_bytes, uint32_t max_chunks, uint32_t max_uploads,
-                            bool (*reclaim)(void*), void* reclaim_arg, efes_queue** out);
+                            bool (*reclaim)(void*, uint32_t want), void* reclaim_arg, efes_queue** out);
 uint64_t queue_reclaims(efes_queue* q);  // reclaim calls so far
 
 // ---- fused digest pairs (efes_stream.cpp on efes_queue.cpp) ----------------------------------
 // io.MultiWriter(f, CRC32, Sha1) (filereceiver.go:208) hands the same bytes to a CRC digest and
 // then to a SHA-1 digest; the digest layer binds such a pair to ONE upload that keeps both hashes.
-// The leader's (CRC) Write stages its bytes without handing them to the dispatcher; the follower's
-// (SHA-1) identical Write is checked against the staged bytes and confirms them.
-uint64_t upload_chunk_bytes(const efes_upload* u);
-// u holds exactly n staged bytes in its current chunk and nothing queued or running (its first Write).
-bool upload_holds_only(efes_upload* u, size_t n);
-// Host address of byte `off` of u's current staging chunk.
-const uint8_t* upload_staged(const efes_upload* u, uint64_t off);
-// u now keeps SHA-1 too: its device SHA-1 state starts from `sha`, the host replay from `shadow`.
-void upload_fuse(efes_upload* u, const efes_sha1_state& sha, const efes_sha1_state& shadow);
+// The leader's (CRC) Write waits in a scratch buffer; the follower's (SHA-1) identical Write is
+// staged and checked against it in one pass, which confirms it.
 // u keeps only `hashes` from now on (a member of a fused pair left it).
 void upload_keep(efes_upload* u, uint32_t hashes);
 // Stages n <= chunk bytes into u's current chunk WITHOUT handing them over (a current chunk without
-// room is handed over first); *off = their offset in the current chunk.  No host replay.  cached:
-// ordinary stores (the bytes are read back on this core next), else streaming stores.
-int upload_stage(efes_upload* u, const void* p, size_t n, uint64_t* off, bool cached);
-// upload_stage with streaming stores that checks the bytes against `ref` in the same pass: they
-// count as staged (fill advances, *off set) only when *same.
+// room is handed over first), with streaming stores that check the bytes against `ref` in the same
+// pass: they count as staged (fill advances, *off = their offset in the chunk) only when *same.  No
+// host replay.
 int upload_stage_if_same(efes_upload* u, const void* p, const void* ref, size_t n, uint64_t* off, bool* same);
 // Bytes the current staging chunk can still take (a whole chunk when there is none or it is full).
 uint64_t upload_room(const efes_upload* u);
@@ -89,8 +81,6 @@ uint64_t upload_room(const efes_upload* u);
 void upload_set_shadow(efes_upload* u, const efes_sha1_state& shadow);
 // The follower matched the staged bytes: its replayed Go state; a full chunk is handed over.
 int upload_confirm(efes_upload* u, const efes_sha1_state& shadow);
-// Drops the staged bytes of the current chunk from offset `off` on (never handed over).
-void upload_truncate(efes_upload* u, uint64_t off);
 // Hands u's partly filled current chunk to the dispatcher (the caller owns u: no call on it runs);
 // false when u holds none.
 bool upload_handover(efes_upload* u);
@@ -131,10 +121,7 @@ hipError_t launch_fill(void* dst, size_t bytes, uint64_t seed, hipStream_t s);
 // workgroup's combine operator as a kernel argument), and the per-context operator tables:
 // row_shift advances a raw register over one workgroup row (kSpanLanes lines), byte-sliced;
 // lane_op[k] = x^(8*kSpanLine*k) mod P.
-#ifndef EFES_SPAN_LINE
-#define EFES_SPAN_LINE 64
-#endif
-constexpr int kSpanLine = EFES_SPAN_LINE;  // bytes per lane per row (A/B: 16, 32, 48, 64, 128)
+constexpr int kSpanLine = 64;  // bytes per lane per row (round 2 A/B of 16, 32, 48, 64, 128: profiles/r02_span/)
 constexpr int kSpanLanes = 1024;
 constexpr int kSpanMaxGroups = 512;
 struct SpanTables {

@@ -820,13 +820,9 @@ struct FedCfg {
   static_assert(kLG > 0 && C >= 1 && C <= 3, "G in {4, 8}, 1..3 chain waves");
 };
 
-// FED4E: raw schedule words W[0..kFedHand-1] the producer hands over (it computes W[16..] of
-// them); the chain wave expands W[kFedHand..79] and adds K.
-#ifndef EFES_FED_HAND
-#define EFES_FED_HAND 16
-#endif
-constexpr int kFedHand = EFES_FED_HAND;
-static_assert(kFedHand >= 16 && kFedHand <= 80 && kFedHand % 4 == 0, "whole uint4 of raw words");
+// FED4E: the producer hands over the 16 message words W[0..15] (big-endian); the chain wave
+// expands W[16..79] and adds K.  (Round 2 measured handing over more of the schedule: no gain.)
+constexpr int kFedHand = 16;
 
 struct FedSlot {
   uint4 wk[20][64];   // [word quad][lane], as PipeSlot
@@ -859,14 +855,6 @@ struct FedLDS {
   uint8_t xs[C][kJobs][64];
   uint8_t fin[C][192];
 };
-
-#ifdef EFES_FED_STATS
-// Diagnostic build only (tools/fed_stats.py): per-wave cycle counts of workgroup 0.
-__device__ unsigned long long g_fed_stats[16];
-#define FED_STAT(...) __VA_ARGS__
-#else
-#define FED_STAT(...)
-#endif
 
 // Counters run modulo 2^32: "a has reached b".
 __device__ __forceinline__ bool reached(uint32_t a, uint32_t b) { return (int32_t)(a - b) >= 0; }
@@ -969,7 +957,6 @@ __device__ __forceinline__ void fed_produce(FedLDS<G, C>& L, int c, int lane, Fe
 template <int G, int C, bool X>
 __device__ void fed_producer(FedLDS<G, C>& L, int lane, int p, uint32_t nchains) {
   constexpr int kP = FedCfg<G, C>::kProducers;
-  FED_STAT(unsigned long long t_prod = 0, n_prod = 0; const unsigned long long t_begin = __builtin_amdgcn_s_memtime();)
   FedFeed F[C];
 #pragma unroll
   for (int c = 0; c < C; ++c) {
@@ -994,40 +981,23 @@ __device__ void fed_producer(FedLDS<G, C>& L, int lane, int p, uint32_t nchains)
         }
       }
       if ((F[c].flags & 1u) && !reached(lds_acq32(&P.taken), F[c].gstep)) continue;  // slot still in use
-      FED_STAT(const unsigned long long t0 = __builtin_amdgcn_s_memtime();)
       fed_produce<G, C, X>(L, c, lane, F[c]);
-      FED_STAT(t_prod += __builtin_amdgcn_s_memtime() - t0; ++n_prod;)
       did = true;
     }
     if (all_done) break;
     if (!did) __builtin_amdgcn_s_sleep(1);
   }
-#ifdef EFES_FED_STATS
-  if (blockIdx.x == 0 && lane == 0 && p == 0) {
-    unsigned hw;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-    g_fed_stats[12] = t_prod;
-    g_fed_stats[13] = n_prod;
-    g_fed_stats[14] = __builtin_amdgcn_s_memtime() - t_begin;
-    g_fed_stats[15] = hw;
-  }
-#endif
 }
 
 // Chain side of one round: S super-steps of G blocks for every joint job of the wave.
 template <int G, bool X>
-__device__ void fed_consume(FedSlot& P, int lane, const DeepMsg* msgs, uint64_t S, uint32_t& gstep, uint32_t (&hv)[5],
-                            unsigned long long* stats) {
-  (void)stats;
+__device__ void fed_consume(FedSlot& P, int lane, const DeepMsg* msgs, uint64_t S, uint32_t& gstep, uint32_t (&hv)[5]) {
   const DeepMsg& M = msgs[lane / G];
 #pragma unroll
   for (int k = 0; k < 5; ++k) hv[k] = M.h[k];
   uint32_t hs[5] = {0, 0, 0, 0, 0};
-  FED_STAT(const unsigned long long t_begin = __builtin_amdgcn_s_memtime();)
   for (uint64_t st = 0; st < S; ++st) {
-    FED_STAT(const unsigned long long t0 = __builtin_amdgcn_s_memtime();)
     while (!reached(lds_acq32(&P.ready), gstep + 1)) __builtin_amdgcn_s_sleep(1);
-    FED_STAT(stats[0] += __builtin_amdgcn_s_memtime() - t0;)
     uint32_t x[80];
     if constexpr (X) {
       uint32_t w[kFedHand];
@@ -1057,7 +1027,6 @@ __device__ void fed_consume(FedSlot& P, int lane, const DeepMsg* msgs, uint64_t 
 #pragma unroll
     for (int k = 0; k < 5; ++k) hv[k] = group_last<G>(hs[k], lane);
   }
-  FED_STAT(stats[1] += __builtin_amdgcn_s_memtime() - t_begin; stats[2] += S;)
 }
 
 template <int G, int C, bool X>
@@ -1105,7 +1074,6 @@ __global__ __launch_bounds__(256, 1) void fed_kernel(const efes_job* __restrict_
   // Joint rounds as in group_kernel, but down to a single job: a lone job still runs at the fed
   // chain's latency, and afterwards every job has fewer than G bulk blocks left.
   uint32_t gstep = 0;
-  unsigned long long stats[3] = {0, 0, 0};
   for (uint32_t round = 0; round < (uint32_t)kJobs; ++round) {
     uint64_t S = ~0ull;
     int joiners = 0;
@@ -1132,7 +1100,7 @@ __global__ __launch_bounds__(256, 1) void fed_kernel(const efes_job* __restrict_
     }
     lds_rel32(&P.req, round + 1);  // release: the messages and S above are visible first
     uint32_t hv[5] = {0, 0, 0, 0, 0};
-    if (any_sha) fed_consume<G, X>(P, lane, msgs, S, gstep, hv, stats);
+    if (any_sha) fed_consume<G, X>(P, lane, msgs, S, gstep, hv);
     while (!reached(lds_acq32(&P.crc_done), round + 1)) __builtin_amdgcn_s_sleep(1);
     const int m = lane / G;
     const bool joint = msgs[m].joint != 0;
@@ -1146,16 +1114,6 @@ __global__ __launch_bounds__(256, 1) void fed_kernel(const efes_job* __restrict_
     wave_lds_sync();
   }
   lds_rel32(&P.fin, 1);
-#ifdef EFES_FED_STATS
-  if (blockIdx.x == 0 && lane == 0) {
-    unsigned hw;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-    g_fed_stats[4 * wave + 0] = stats[0];
-    g_fed_stats[4 * wave + 1] = stats[1];
-    g_fed_stats[4 * wave + 2] = stats[2];
-    g_fed_stats[4 * wave + 3] = hw;
-  }
-#endif
   for (int m = 0; m < kJobs; ++m) {  // per job: the < G left-over blocks, tail, Sum, write-back
     const uint32_t j = j0 + (uint32_t)m;
     if (j >= njobs) break;
@@ -1193,29 +1151,18 @@ constexpr int kWideWaves = 4;    // waves per workgroup per SIMD-wave (one per S
 constexpr int kWideMaxWps = 3;   // waves per SIMD that fit (132 VGPRs)
 constexpr int kXStride = 68;
 
-// WIDE's CRC tables in LDS: the position tables (crc_issue below), or slicing-by-8's.
-#ifndef EFES_WIDE_SLICE8
+// WIDE's CRC tables in LDS: the position tables (crc_issue below).
 using WideCrcTab = uint32_t[64][256];
-#else
-using WideCrcTab = uint32_t[8][256];
-#endif
 
 struct WideLDS {
-  WideCrcTab crc;  // PosTables (64 KiB), or slice8 (8 KiB) with -DEFES_WIDE_SLICE8
+  WideCrcTab crc;  // PosTables (64 KiB)
   uint32_t prog[kWideWaves * kWideMaxWps];  // blocks done by each wave of the workgroup
 };
-#ifndef EFES_WIDE_SLICE8
 // The byte-wise head/tail: pos[63][b] (byte b, no byte after it) is IEEETable[b] (crc32.go:125).
 __device__ __forceinline__ const uint32_t* wide_t0(const WideLDS& L) { return L.crc[63]; }
 __device__ __forceinline__ const uint4* wide_tab_src(const Tables* tabs) {
   return reinterpret_cast<const uint4*>(tabs + 1);  // PosTables follow Tables (efes_ctx_create)
 }
-#else
-__device__ __forceinline__ const uint32_t* wide_t0(const WideLDS& L) { return L.crc[0]; }
-__device__ __forceinline__ const uint4* wide_tab_src(const Tables* tabs) {
-  return reinterpret_cast<const uint4*>(tabs->slice8);
-}
-#endif
 
 // The priority of wave w from its SIMD siblings' progress (w % 4, w % 4 + 4, ...): the furthest
 // behind gets 3, the furthest ahead 0, the rest 1.  Wave-uniform; `b` = blocks this wave has done.
@@ -1260,11 +1207,10 @@ __device__ __forceinline__ uint32_t fin_byte(const uint8_t* xl, uint32_t i, uint
 // previous block.  Split in eight groups of eight bytes (LE words 2S, 2S+1): a group's lookups are
 // issued first, the XORs that fold them into the running value come five SHA-1 rounds later.
 // 97 VALU per block (64 lookup addresses, 1 + 32 XORs) against 112 for slicing-by-8's eight
-// dependent steps (`-DEFES_WIDE_SLICE8`, kept for A/B).
+// dependent steps (round 3 A/B, profiles/r03_wide_crc_ab/).
 struct CrcPending {
   uint32_t v[8];
 };
-#ifndef EFES_WIDE_SLICE8
 template <int S>
 __device__ __forceinline__ void crc_issue(const WideCrcTab& t, uint32_t crc, const uint32_t (&le)[16], CrcPending& p) {
   const uint32_t lo = S == 0 ? crc ^ le[0] : le[2 * S];
@@ -1283,23 +1229,6 @@ __device__ __forceinline__ uint32_t crc_combine(const CrcPending& p, uint32_t ac
   const uint32_t c = __builtin_amdgcn_bitop3_b32(acc, a, b, 0x96);
   return __builtin_amdgcn_bitop3_b32(c, p.v[6], p.v[7], 0x96);
 }
-#else
-// One slicing-by-8 step (8 bytes = LE words 2S, 2S+1) of crc_words_raw.
-template <int S>
-__device__ __forceinline__ void crc_issue(const WideCrcTab& t, uint32_t crc, const uint32_t (&le)[16], CrcPending& p) {
-  const uint32_t hi = le[2 * S + 1];
-  const uint32_t c = crc ^ le[2 * S];
-  p.v[0] = t[0][hi >> 24]; p.v[1] = t[1][(hi >> 16) & 0xffu]; p.v[2] = t[2][(hi >> 8) & 0xffu];
-  p.v[3] = t[3][hi & 0xffu]; p.v[4] = t[4][c >> 24]; p.v[5] = t[5][(c >> 16) & 0xffu];
-  p.v[6] = t[6][(c >> 8) & 0xffu]; p.v[7] = t[7][c & 0xffu];
-}
-template <int S>
-__device__ __forceinline__ uint32_t crc_combine(const CrcPending& p, uint32_t) {
-  const uint32_t a = __builtin_amdgcn_bitop3_b32(p.v[0], p.v[1], p.v[2], 0x96);
-  const uint32_t b = __builtin_amdgcn_bitop3_b32(p.v[3], p.v[4], p.v[5], 0x96);
-  return __builtin_amdgcn_bitop3_b32(a, b, p.v[6] ^ p.v[7], 0x96);
-}
-#endif
 
 // 80 inline SHA-1 rounds with the 8 CRC groups of the same block woven in: group k's lookups are
 // issued after round 10k+4 and combined after round 10k+9, so the LDS latency of the lookups is
@@ -1368,7 +1297,6 @@ __device__ __forceinline__ void wide_bulk(const uint8_t* q, uint64_t nbulk, uint
   load_block_le<kAligned16>(src(0), A);
   load_block_le<kAligned16>(src(1), B);
   uint64_t b = 0;
-#ifndef EFES_WIDE_BLOCKLOADS
   // Uniform phase (blocks b..b+5 exist in every lane), a 128-B line at a time: the two blocks of a
   // line are loaded back to back (eight dwordx4), one block-time before the first is hashed.  A
   // lane's blocks loaded one at a time, a block apart (the A/B build below), fetched 14.5 % more
@@ -1387,20 +1315,10 @@ __device__ __forceinline__ void wide_bulk(const uint8_t* q, uint64_t nbulk, uint
     load_block_le<kAligned16>(qb + 320, B);
     wide_step<kSha, kCrc>(C, t, h, crc_raw, true);
   }
-#else
-  for (; b + 4 < nmin; b += 3) {  // uniform phase: blocks b..b+4 exist in every lane
-    if (b % 6 == 0) wide_pace(prog, w, nw, (uint32_t)b);  // every 6 blocks: ~4 VALU per block
-    const uint8_t* qb = q + 64 * b;
-    load_block_le<kAligned16>(qb + 128, C);
-    wide_step<kSha, kCrc>(A, t, h, crc_raw, true);
-    load_block_le<kAligned16>(qb + 192, A);
-    wide_step<kSha, kCrc>(B, t, h, crc_raw, true);
-    load_block_le<kAligned16>(qb + 256, B);
-    wide_step<kSha, kCrc>(C, t, h, crc_raw, true);
-  }
-#endif
-  for (; b < nmax; b += 3) {  // ragged phase (A, B hold blocks b, b+1 or the dummy)
-    if (b % 6 == 0) wide_pace(prog, w, nw, (uint32_t)b);
+  // ragged phase (A, B hold blocks b, b+1 or the dummy), paced at its start and every 6 blocks
+  // (counted from the start: b enters at a multiple of 4, so b % 6 alone could skip every pace)
+  for (const uint64_t b_ragged = b; b < nmax; b += 3) {
+    if ((b - b_ragged) % 6 == 0) wide_pace(prog, w, nw, (uint32_t)b);
     load_block_le<kAligned16>(src(b + 2), C);
     wide_step<kSha, kCrc>(A, t, h, crc_raw, b < nbulk);
     if (b + 1 >= nmax) break;
@@ -1443,19 +1361,10 @@ __device__ __forceinline__ uint64_t wave_max64(uint64_t v) {
   return uniform64(v);
 }
 
-#ifdef EFES_WIDE_STATS
-// Diagnostic build (tools/wide_stats.py): per wave of the last launch, s_memtime at entry, after
-// the bulk loop and at exit, HW_ID and XCC_ID -- the timeline of the waves sharing each SIMD.
-__device__ unsigned long long g_wide_stats[8192 * 6];
-#endif
 
 __global__ __launch_bounds__(64 * kWideWaves * kWideMaxWps, 1) void wide_kernel(const efes_job* __restrict__ jobs,
                                                                                 uint32_t njobs,
                                                                                 const Tables* __restrict__ tabs) {
-#ifdef EFES_WIDE_STATS
-  const unsigned long long st_t0 = __builtin_amdgcn_s_memtime();
-  const unsigned long long st_r0 = __builtin_amdgcn_s_memrealtime();
-#endif
   __shared__ __attribute__((aligned(16))) WideLDS L;
   extern __shared__ __attribute__((aligned(16))) uint8_t wide_xs[];  // blockDim.x x kXStride (launch_wide)
   {
@@ -1534,9 +1443,6 @@ __global__ __launch_bounds__(64 * kWideWaves * kWideMaxWps, 1) void wide_kernel(
   if (all16) wide_bulk_any<true>(q, nbulk, nmin, nmax, dummy, any_sha, any_crc, L.crc, h, crc_raw, L.prog, wv, nwv);
   else wide_bulk_any<false>(q, nbulk, nmin, nmax, dummy, any_sha, any_crc, L.crc, h, crc_raw, L.prog, wv, nwv);
   if ((threadIdx.x & 63) == 0) __atomic_store_n(&L.prog[wv], 0xffffffffu, __ATOMIC_RELAXED);  // done: never the slowest
-#ifdef EFES_WIDE_STATS
-  const unsigned long long st_t1 = __builtin_amdgcn_s_memtime();
-#endif
 
   // ---- tail
   const uint64_t tpos = pos + (nbulk << 6);
@@ -1597,25 +1503,8 @@ __global__ __launch_bounds__(64 * kWideWaves * kWideMaxWps, 1) void wide_kernel(
     }
   }
   if (live && jb.status) *jb.status = bad ? EFES_ERR_STATE : status;
-#ifdef EFES_WIDE_STATS
-  const unsigned long long st_t2 = __builtin_amdgcn_s_memtime();
-  const uint32_t gw = (blockIdx.x * blockDim.x + threadIdx.x) / 64;
-  if ((threadIdx.x & 63) == 0 && gw < 8192) {
-    uint32_t hw, xcc;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    const unsigned long long st_r2 = __builtin_amdgcn_s_memrealtime();
-    unsigned long long* o = g_wide_stats + 6 * gw;
-    o[0] = st_t0; o[1] = st_t1; o[2] = st_t2; o[3] = hw; o[4] = xcc; o[5] = (st_r2 - st_r0) << 32 | (st_r0 & 0xffffffffull);
-  }
-#endif
 }
 
-#ifdef EFES_WIDE_STATS
-extern "C" int efes_debug_wide_stats(unsigned long long* out) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wide_stats), sizeof(g_wide_stats)) == hipSuccess ? 0 : -3;
-}
-#endif
 
 // ================================================================== synthetic fill
 __device__ __forceinline__ uint64_t splitmix(uint64_t seed, uint64_t i) {
@@ -1689,27 +1578,17 @@ hipError_t launch_fed_shape(const efes_job* jobs, uint32_t njobs, const Tables* 
 
 hipError_t launch_fed(const efes_job* jobs, uint32_t njobs, const Tables* tabs, hipStream_t s, bool expand) {
   if (njobs == 0) return hipSuccess;
-  if (const char* e = getenv("EFES_FED_SHAPE")) {  // developer override for calibration: "G,C"
-    if (!strcmp(e, "4,3")) return launch_fed_shape<4, 3>(jobs, njobs, tabs, s);
-    if (!strcmp(e, "8,3")) return launch_fed_shape<8, 3>(jobs, njobs, tabs, s);
-  }
   if (expand) return launch_fed_shape<4, 3, true>(jobs, njobs, tabs, s);  // FED4E
   return launch_fed_shape<kFed4G, kFed4C>(jobs, njobs, tabs, s);          // FED4
 }
-
-// EFES_WIDE_PACE=0 (A/B): read once, when the library is loaded.
-static const bool g_wide_pace_off = [] {
-  const char* e = getenv("EFES_WIDE_PACE");
-  return e && *e == '0';
-}();
 
 hipError_t launch_wide(const efes_job* jobs, uint32_t njobs, const Tables* tabs, hipStream_t s, bool exclusive,
                        int cus) {
   if (njobs == 0) return hipSuccess;
   // waves per SIMD of the launch: a workgroup per CU holds all of its SIMDs' waves (wide_pace);
-  // exclusive parts (one wave per SIMD on reserved CUs) and EFES_WIDE_PACE=0 use 4-wave groups.
+  // exclusive parts (one wave per SIMD on reserved CUs) use 4-wave groups.
   const uint64_t waves = (njobs + 63) / 64, simds = 4ull * (uint64_t)(cus > 0 ? cus : 256);
-  const uint32_t wps = exclusive || g_wide_pace_off ? 1u : (uint32_t)std::min<uint64_t>(kWideMaxWps, (waves + simds - 1) / simds);
+  const uint32_t wps = exclusive ? 1u : (uint32_t)std::min<uint64_t>(kWideMaxWps, (waves + simds - 1) / simds);
   const uint32_t per = 64 * kWideWaves * wps;
   const size_t xs = (size_t)per * kXStride;  // the lanes' tail buffers (dynamic LDS)
   // The kernel's static LDS, and the dynamic-LDS limit raised once to the rest of the CU's LDS
@@ -1743,12 +1622,6 @@ hipError_t launch_wide(const efes_job* jobs, uint32_t njobs, const Tables* tabs,
   hipLaunchKernelGGL(wide_kernel, dim3((njobs + per - 1) / per), dim3(per), dyn, s, jobs, njobs, tabs);
   return hipGetLastError();
 }
-
-#ifdef EFES_FED_STATS
-extern "C" int efes_debug_fed_stats(unsigned long long* out) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fed_stats), sizeof(g_fed_stats)) == hipSuccess ? 0 : -3;
-}
-#endif
 
 hipError_t launch_fill(void* dst, size_t bytes, uint64_t seed, hipStream_t s) {
   const uint64_t nwords = bytes / 8;

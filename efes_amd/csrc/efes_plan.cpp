@@ -320,36 +320,6 @@ int efes_plan_batch(efes_ctx* ctx, const uint64_t* lengths, uint32_t n, uint32_t
   }
   if (n > prev) parts[np++] = efes_plan_part{n - prev, EFES_MODE_WIDE, 0u, 0u};
 
-  // Developer override for calibration runs:
-  //   EFES_PLAN_FORCE="<lanes>:<jobs>[x],<lanes>:<jobs>[x],..."  (lanes 64 = DEEP, 0 = WIDE,
-  //   1 = FED4, 2 = FED4E (both always exclusive), x = exclusive); jobs beyond the listed parts run
-  //   WIDE (a part beyond EFES_PLAN_MAX_PARTS is not possible).
-  if (const char* f = getenv("EFES_PLAN_FORCE"); f && *f) {
-    efes_plan_part fp[EFES_PLAN_MAX_PARTS] = {};
-    uint32_t fn = 0, used = 0;
-    bool ok = true;
-    for (const char* c = f; *c && ok;) {
-      int g = -1, len = 0;
-      unsigned long long d = 0;
-      ok = sscanf(c, "%d:%llu%n", &g, &d, &len) == 2 && lanes_of(mode_of(g)) == g && fn < EFES_PLAN_MAX_PARTS;
-      if (!ok) break;
-      c += len;
-      const bool x = *c == 'x';
-      c += x;
-      c += *c == ',';
-      const uint32_t take = (uint32_t)std::min<unsigned long long>(d, n - used);
-      if (take) fp[fn++] = efes_plan_part{take, mode_of(g), x ? 1u : 0u, 0u};
-      used += take;
-    }
-    if (ok && used < n) {
-      if (fn < EFES_PLAN_MAX_PARTS) fp[fn++] = efes_plan_part{n - used, EFES_MODE_WIDE, 0u, 0u};
-      else ok = false;
-    }
-    if (ok) {
-      np = fn;
-      std::copy(fp, fp + fn, parts);
-    }
-  }
   plan->nparts = np;
   std::copy(parts, parts + np, plan->part);
   plan->est_seconds = best_t / kClock;

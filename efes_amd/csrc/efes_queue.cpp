@@ -101,15 +101,15 @@ struct efes_queue {
   // when writers wait for a chunk, none is free and nothing is queued, the dispatcher calls it --
   // without mu, holding no lock of the owner layer -- to have idle uploads hand their partly
   // filled chunks over, so no writer waits on chunks that nobody would hand over.
-  bool (*reclaim)(void*) = nullptr;
+  bool (*reclaim)(void*, uint32_t want) = nullptr;
   void* reclaim_arg = nullptr;
   uint32_t chunk_waiters = 0;      // writers blocked in take_chunk
   uint64_t n_reclaims = 0;
   bool starving() const { return reclaim && chunk_waiters > 0 && free_chunks.empty(); }
   // hipEventBlockingSync: the dispatcher sleeps in retire instead of polling the event, so it does
   // not keep a host core busy beside the request threads (receiver within noise either way:
-  // profiles/r03_receiver/ab_sync_*.log); EFES_QUEUE_SYNC=spin restores the poll.
-  unsigned ev_flags = hipEventDisableTiming | hipEventBlockingSync;
+  // profiles/r03_receiver/ab_sync_*.log).
+  static constexpr unsigned ev_flags = hipEventDisableTiming | hipEventBlockingSync;
   std::thread th;
 
   void run();
@@ -143,8 +143,9 @@ void efes_queue::run() {
         // in an upload.  Have the idle holders hand theirs over, so the next launch is assembled
         // while the running one finishes.
         ++n_reclaims;
+        const uint32_t want = chunk_waiters;  // > 0 (starving)
         lk.unlock();
-        const bool any = reclaim(reclaim_arg);
+        const bool any = reclaim(reclaim_arg, want);
         lk.lock();
         if (any) continue;
         if (running.empty()) {  // holders busy, nothing to retire: look again soon
@@ -281,7 +282,7 @@ int take_chunk(efes_upload* u, std::unique_lock<std::mutex>& lk) {
 // gains nothing from more (its chain takes one chunk per launch: one in the running launch, one
 // in the launch queued behind it, one pending for the launch after), while a fast writer that
 // grabs every free chunk leaves the other uploads nothing to put in the next launches.
-// EFES_QUEUE_AHEAD overrides kAhead (0: no per-upload cap).  "Scarce" = no more free chunks than
+// "Scarce" = no more free chunks than
 // uploads OPEN now (each may need one to go on), not than the queue's capacity: the shared digest
 // queue has max_uploads = chunks - 1, so a capacity test paced every digest always -- and its
 // writers then slept and woke once per 64 KiB chunk (drainer at 512 files: 17-19 GiB/s paced from
@@ -382,7 +383,7 @@ int efes_queue_create(efes_ctx* ctx, uint64_t chunk_bytes, uint32_t max_chunks, 
 }  // extern "C"
 
 int efes::queue_create_reclaiming(efes_ctx* ctx, uint64_t chunk_bytes, uint32_t max_chunks, uint32_t max_uploads,
-                                  bool (*reclaim)(void*), void* reclaim_arg, efes_queue** out) {
+                                  bool (*reclaim)(void*, uint32_t), void* reclaim_arg, efes_queue** out) {
   if (!ctx || !out || max_chunks < 2 || max_uploads == 0 || (max_uploads >= max_chunks && !reclaim))
     return EFES_ERR_ARG;
   *out = nullptr;
@@ -394,9 +395,7 @@ int efes::queue_create_reclaiming(efes_ctx* ctx, uint64_t chunk_bytes, uint32_t 
   q->max_uploads = max_uploads;
   q->reclaim = reclaim;
   q->reclaim_arg = reclaim_arg;
-  const char* ah = getenv("EFES_QUEUE_AHEAD");
-  q->ahead = ah && *ah ? strtoull(ah, nullptr, 10) : kAhead;
-  if (const char* qs = getenv("EFES_QUEUE_SYNC"); qs && !strcmp(qs, "spin")) q->ev_flags = hipEventDisableTiming;
+  q->ahead = kAhead;
   DeviceGuard g(ctx->device);
   hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&q->h_slab), q->chunk * max_chunks, hipHostMallocMapped);
   if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void**>(&q->z_slab), q->h_slab, 0);
@@ -672,31 +671,12 @@ efes_sha1_state upload_shadow(const efes_upload* u) { return u->shadow; }
 
 // ---- fused digest pairs (efes_internal.hpp; used by efes_stream.cpp) ----------------------------
 // The caller owns the upload as its writer (cur/fill need no lock, as in efes_upload_write).
-uint64_t upload_chunk_bytes(const efes_upload* u) { return u->q->chunk; }
-
 uint64_t upload_room(const efes_upload* u) {
   const uint64_t c = u->q->chunk;
   return u->cur >= 0 && u->fill < c ? c - u->fill : c;
 }
 
 void upload_set_shadow(efes_upload* u, const efes_sha1_state& shadow) { u->shadow = shadow; }
-
-bool upload_holds_only(efes_upload* u, size_t n) {
-  std::lock_guard<std::mutex> lk(u->q->mu);
-  return !u->latched && u->inflight == 0 && u->queued == 0 && u->cur >= 0 && u->fill == n && !u->fold_sum;
-}
-
-const uint8_t* upload_staged(const efes_upload* u, uint64_t off) {
-  return u->q->h_slab + (size_t)u->cur * u->q->chunk + off;
-}
-
-void upload_fuse(efes_upload* u, const efes_sha1_state& sha, const efes_sha1_state& shadow) {
-  std::lock_guard<std::mutex> lk(u->q->mu);  // the dispatcher reads `hashes` when it assembles a batch
-  u->hashes = EFES_HASH_SHA1 | EFES_HASH_CRC32;
-  // no job of u is queued or running (upload_holds_only): the slot is ours to write
-  memcpy(u->q->h_states + (size_t)u->dslot * kDevStateBytes, &sha, sizeof sha);
-  u->shadow = shadow;
-}
 
 void upload_keep(efes_upload* u, uint32_t hashes) {
   std::lock_guard<std::mutex> lk(u->q->mu);
@@ -705,27 +685,6 @@ void upload_keep(efes_upload* u, uint32_t hashes) {
     memset(&u->shadow, 0, sizeof u->shadow);
     efes_sha1_state_init(&u->shadow);
   }
-}
-
-int upload_stage(efes_upload* u, const void* p, size_t n, uint64_t* off, bool cached) {
-  if (u->latched) return u->latched;
-  efes_queue* q = u->q;
-  if (u->cur >= 0 && u->fill + n > q->chunk) {  // no room: hand the (matched) chunk over first
-    std::unique_lock<std::mutex> lk(q->mu);
-    enqueue_current(u, lk);
-    pace(u, lk);
-  }
-  if (u->cur < 0) {
-    std::unique_lock<std::mutex> lk(q->mu);
-    if (int rc = take_chunk(u, lk)) return rc;
-    u->fill = 0;
-  }
-  uint8_t* dst = q->h_slab + (size_t)u->cur * q->chunk + u->fill;
-  if (cached) memcpy(dst, p, n);
-  else copy_to_staging(dst, static_cast<const uint8_t*>(p), n);
-  *off = u->fill;
-  u->fill += n;
-  return EFES_OK;
 }
 
 int upload_stage_if_same(efes_upload* u, const void* p, const void* ref, size_t n, uint64_t* off, bool* same) {
@@ -775,9 +734,6 @@ uint64_t queue_reclaims(efes_queue* q) {
   return q->n_reclaims;
 }
 
-void upload_truncate(efes_upload* u, uint64_t off) {
-  if (u->cur >= 0 && off < u->fill) u->fill = off;
-}
 }  // namespace efes
 
 extern "C" {

@@ -23,20 +23,21 @@
 // FUSED PAIRS (round 4).  MultiWriter(f, CRC32, Sha1) (filereceiver.go:208-209, fileinfo.go:20-27)
 // hands every body buffer p to the CRC digest and then, unchanged, to the SHA-1 digest.  Two
 // separate uploads would stage p twice and launch two jobs that each read it over PCIe.  Instead:
-//   * a CRC digest whose Write opened a fresh upload registers that Write (p, n) as a candidate;
-//   * a parked SHA-1 digest whose Write has the same (p, n) BINDS to it if the candidate's staged
-//     bytes equal p (memcmp): the upload then keeps both hashes, the SHA-1 state slot starts from
-//     the SHA-1 digest's parked state, and nothing is staged for the SHA-1 Write;
-//   * after that the leader's (CRC) Write stages its bytes but does not hand them to the
-//     dispatcher; the follower's (SHA-1) Write of the same (p, n) is checked against them (memcmp)
-//     and confirms them -- one staging copy and one fused job per body byte;
+//   * a CRC digest's first Write after a sync point waits in a scratch buffer and registers (p, n)
+//     as a candidate;
+//   * a parked SHA-1 digest whose Write has the same (p, n) BINDS to it: the pair opens ONE upload
+//     keeping both hashes (SHA-1 from the SHA-1 digest's parked state, CRC from the CRC digest's)
+//     and the waiting Write becomes the pair's open leader Write;
+//   * from then on the leader's (CRC) Write waits in a cache-hot scratch buffer; the follower's
+//     (SHA-1) Write of the same (p, n) is staged with streaming stores and compared with it in the
+//     same pass, which confirms it -- one staging copy and one fused job per body byte;
 //   * anything else -- a Write to one digest only, different bytes, a Sum / MarshalText of the
 //     leader first, Reset / UnmarshalText / free of one, an eviction -- SETTLES the pair: every
 //     confirmed byte is hashed into both states, the leader's unconfirmed bytes into its state
 //     only, and both digests continue alone (a follower's sync point or a member whose state is
 //     being replaced just LEAVES, the partner keeping the upload).
 // So a wrong guess costs time, never correctness: every digest hashes exactly the bytes of its
-// own Writes, in order.  EFES_DIGEST_FUSE=0 disables binding (A/B).
+// own Writes, in order.
 //
 // Placement: a digest made on a context uses that context's queue; one made on a pool
 // (efes_pool_create) opens each upload on the pool's context with the most free slots, skipping
@@ -78,8 +79,8 @@ struct Digest {
   const void* cand_p = nullptr;  // a CRC digest whose upload holds exactly its first Write (cand_p, cand_n)
   size_t cand_n = 0;
   std::atomic<int64_t> last_ns{0};  // end of its last call (eviction prefers long-idle holders)
-  // EFES_PAIR_STAGE=scratch: a CRC digest's first Write on a fresh upload waits here, as the
-  // candidate, until a SHA-1 digest binds to it or the digest's next call stages it
+  // a CRC digest's first Write after a sync point waits here, as the candidate, until a SHA-1
+  // digest binds to it or the digest's next call stages it
   uint8_t* defer = nullptr;
   size_t defer_cap = 0, defer_n = 0;
   bool sha() const { return hashes == EFES_HASH_SHA1; }
@@ -95,18 +96,16 @@ struct Fused {
   std::list<OpenRef>::iterator pos;  // in on->dreg.open while u != nullptr
   bool lead_in = true, follow_in = true;  // members still sharing the upload
   int refs = 2;                    // members whose fz still points here
-  // the leader's last Write: staged in u's current chunk, not yet matched by the follower
+  // the leader's last Write, waiting in `scratch`, not yet matched by the follower
   bool open = false;
   const void* op = nullptr;
   size_t on_bytes = 0;
-  uint64_t ooff = 0;
   // after settle(): both states after every byte, for the members to pick up at their next call
   bool settled = false;
   efes_sha1_state sha_out{};
   efes_crc32_state crc_out{};
   int rc_sha = EFES_OK, rc_crc = EFES_OK;
   std::atomic<int64_t> last_ns{0};  // end of a member's last call on the pair
-  // EFES_PAIR_STAGE=scratch: the leader's open Write waits here instead of in the upload
   uint8_t* scratch = nullptr;
   size_t scratch_cap = 0;
   size_t conf = 0;  // bytes of the open scratch Write the follower has confirmed (staged in pieces)
@@ -146,46 +145,29 @@ int64_t now_ns() {
   return (int64_t)ts.tv_sec * 1000000000ll + ts.tv_nsec;
 }
 
-// Eviction patience: a Write that finds every slot taken first waits for a holder's sync point and
-// evicts only holders idle for this long (a stalled client, an abandoned digest); once it has
-// waited this long itself it evicts the oldest idle holder, active or not (progress).  Evicting
-// active holders at once made every Write of an over-subscribed queue settle another upload and
-// wait for the GPU (EFES_DIGEST_EVICT_MS=0 restores that).
+// Eviction patience (EFES_DIGEST_EVICT_MS, default 50): a Write that finds every slot taken first
+// waits for a holder's sync point and evicts only holders idle for this long (a stalled client, an
+// abandoned digest); once it has waited this long itself it evicts the oldest idle holder, active or
+// not (progress).  Evicting active holders at once (0) made every Write of an over-subscribed queue
+// settle another upload and wait for the GPU (profiles/r04_evict/evict.log).  Read once when the
+// library is loaded (by one thread, before any call): a function-local static initialised on first
+// use is first read by request threads racing each other.
+const int64_t g_evict_patience_ns = [] {
+  const char* e = getenv("EFES_DIGEST_EVICT_MS");
+  return (e && *e ? strtoll(e, nullptr, 10) : 50ll) * 1000000ll;
+}();
 
-// Where the leader's Write waits for the follower's (EFES_PAIR_STAGE):
-//   scratch -- (default) copied into a cache-hot per-thread scratch buffer; the follower's Write
-//              stages with streaming stores while comparing against it in the same pass (no
-//              read-for-ownership of the staging lines, no second pass over the bytes);
-//   cached  -- staged in the upload with ordinary stores, so the follower's memcmp hits the cache;
-//   stream  -- staged with the streaming stores of every other Write: the memcmp reads DRAM.
-// Interleaved on one box (profiles/r04_pair_stage_ab2/ab.log): scratch 46.8-47.7, cached 45.9-46.4,
-// stream 46.3-47.5 GiB/s, efes_upload 48.9-49.3; on another (r04_pair_stage_ab) stream ran 35.2-39.8
-// against cached 43.5-43.7.
-enum class PairStage { kCached, kStream, kScratch };
+int64_t evict_patience_ns() { return g_evict_patience_ns; }
 
-// The environment switches above, read once when the library is loaded (by one thread, before any
-// call): function-local statics initialised on first use are first read by request threads racing
-// each other.
-struct Env {
-  int64_t evict_patience_ns = 50 * 1000000ll;
-  bool fuse = true;
-  PairStage stage = PairStage::kScratch;
-  Env() {
-    if (const char* e = getenv("EFES_DIGEST_EVICT_MS"); e && *e) evict_patience_ns = strtoll(e, nullptr, 10) * 1000000ll;
-    if (const char* e = getenv("EFES_DIGEST_FUSE"); e && !strcmp(e, "0")) fuse = false;
-    if (const char* e = getenv("EFES_PAIR_STAGE")) {
-      if (!strcmp(e, "stream")) stage = PairStage::kStream;
-      if (!strcmp(e, "cached")) stage = PairStage::kCached;
-    }
-  }
-};
-const Env g_env;
+// Where the leader's Write waits for the follower's: a cache-hot per-thread scratch buffer, so the
+// follower's Write stages with streaming stores while comparing against it in the same pass (no
+// read-for-ownership of the staging lines, no second pass over the bytes).  Round 4 measured the
+// alternatives -- the leader staged in the upload with ordinary stores (the compare hits the cache,
+// every staging line is read for ownership first) or with streaming stores (the compare reads DRAM):
+// scratch 46.8-47.7, cached 45.9-46.4, stream 46.3-47.5 GiB/s against efes_upload 48.9-49.3
+// (profiles/r04_pair_stage_ab2/ab.log), and removed them in round 5.
 
-int64_t evict_patience_ns() { return g_env.evict_patience_ns; }
-bool fuse_enabled() { return g_env.fuse; }
-PairStage pair_stage() { return g_env.stage; }
-
-// Scratch buffers for PairStage::kScratch: a few per thread, reused last-in first-out so the one a
+// Scratch buffers: a few per thread, reused last-in first-out so the one a
 // leader Write copies into is still in this core's cache when the follower's Write (normally on
 // the same thread, right after) compares against it.  A buffer may be returned on another thread.
 // The per-thread slots are trivially destructible, so a digest call made while the thread is being
@@ -239,7 +221,10 @@ void scratch_put(uint8_t* p, size_t cap) {
 }
 
 
-bool reclaim_chunks(void* arg);
+bool reclaim_chunks(void* arg, uint32_t want);
+
+// Default pinned staging per context, and the floor a failed allocation is retried down to.
+constexpr uint64_t kDigestStagingMib = 1024, kDigestStagingMinMib = 256;
 
 // Shared queue sizing: EFES_DIGEST_STAGING_MIB of pinned staging (default 1024 MiB) in chunks of
 // EFES_DIGEST_CHUNK_KIB (default 256 KiB: 4096 chunks; 256 KiB chunks ran 34.8 against 31.8 GiB/s
@@ -252,7 +237,7 @@ bool reclaim_chunks(void* arg);
 // (settling) another upload.  EFES_DIGEST_SLOTS below the chunks gives round 3's queue (slots =
 // min(EFES_DIGEST_SLOTS, chunks - 1), no reclaim).
 efes_queue* create_digest_queue(efes_ctx* ctx, int* rc) {
-  uint64_t mib = 1024, kib = 256, slots = 65536;
+  uint64_t mib = kDigestStagingMib, kib = 256, slots = 65536;
   if (const char* e = getenv("EFES_DIGEST_STAGING_MIB")) mib = strtoull(e, nullptr, 10);
   if (const char* e = getenv("EFES_DIGEST_CHUNK_KIB")) kib = strtoull(e, nullptr, 10);
   if (const char* e = getenv("EFES_DIGEST_SLOTS")) slots = strtoull(e, nullptr, 10);
@@ -261,12 +246,18 @@ efes_queue* create_digest_queue(efes_ctx* ctx, int* rc) {
   if (slots < 1) slots = 1;
   if (slots > (1u << 22)) slots = 1u << 22;
   const uint64_t chunk = kib << 10;
-  const uint32_t chunks = (uint32_t)((mib << 20) / chunk) < 16 ? 16u : (uint32_t)((mib << 20) / chunk);
   efes_queue* q = nullptr;
-  if (slots >= chunks)
-    *rc = efes::queue_create_reclaiming(ctx, chunk, chunks, (uint32_t)slots, reclaim_chunks, ctx, &q);
-  else
-    *rc = efes_queue_create(ctx, chunk, chunks, (uint32_t)slots, &q);
+  for (;;) {
+    const uint32_t chunks = (uint32_t)((mib << 20) / chunk) < 16 ? 16u : (uint32_t)((mib << 20) / chunk);
+    if (slots >= chunks)
+      *rc = efes::queue_create_reclaiming(ctx, chunk, chunks, (uint32_t)slots, reclaim_chunks, ctx, &q);
+    else
+      *rc = efes_queue_create(ctx, chunk, chunks, (uint32_t)slots, &q);
+    // The pinned staging did not fit (host memory locked by others, a small cgroup): halve it down
+    // to kDigestStagingMinMib before the error is latched into every digest of the context.
+    if (*rc == EFES_OK || (*rc != EFES_ERR_HIP && *rc != EFES_ERR_NOMEM) || mib <= kDigestStagingMinMib) break;
+    mib = std::max<uint64_t>(kDigestStagingMinMib, mib / 2);
+  }
   if (*rc == EFES_OK && ctx->fault_after) efes::queue_set_fault_after(q, ctx->fault_after);
   return *rc == EFES_OK ? q : nullptr;
 }
@@ -348,21 +339,14 @@ void park(Digest* d) {
 }
 
 // ---- fused pairs --------------------------------------------------------------------------------
-// The leader's open Write (what of it the follower has not confirmed): in its scratch buffer, or
-// staged in the upload's current chunk.
-const uint8_t* pending(const Fused* z) {
-  return z->scratch ? z->scratch + z->conf : efes::upload_staged(z->u, z->ooff);
-}
+// The leader's open Write (what of it the follower has not confirmed), in its scratch buffer.
+const uint8_t* pending(const Fused* z) { return z->scratch + z->conf; }
 size_t pending_n(const Fused* z) { return z->on_bytes - z->conf; }
 
 // Gives the leader's open Write up (z->mu held).
 void drop_pending(Fused* z) {
-  if (z->scratch) {
-    scratch_put(z->scratch, z->scratch_cap);
-    z->scratch = nullptr;
-  } else {
-    efes::upload_truncate(z->u, z->ooff);
-  }
+  scratch_put(z->scratch, z->scratch_cap);
+  z->scratch = nullptr;
   z->open = false;
   z->conf = 0;
 }
@@ -449,7 +433,7 @@ int leave(Digest* d, Fused* z, bool sync, std::unique_lock<std::mutex>& zk) {
       if (rc != EFES_OK && d->latched == EFES_OK) d->latched = rc;
     }
     efes::upload_keep(u, EFES_HASH_CRC32);
-    if (z->open && z->scratch) {  // the leader's open Write is its own: into the (now CRC-only) upload
+    if (z->open) {  // the leader's open Write is its own: into the (now CRC-only) upload
       (void)efes_upload_write(u, pending(z), pending_n(z));  // a fault is latched in u
       drop_pending(z);
     }
@@ -530,29 +514,28 @@ struct Call {
   }
 };
 
-// The digest queue's reclaim hook (run by its dispatcher thread, which holds no digest or pair
-// lock): every chunk sits partly filled in an upload while writers wait for one, so each holder
-// that is not inside a call hands its partly filled chunk over (hashed like a full one, then
-// freed).  A fused pair with an unconfirmed leader Write staged in its chunk keeps the chunk: its
-// follower's Write comes next.  Returns whether anything was handed over.
-bool reclaim_chunks(void* arg) {
+// The digest queue's reclaim hook (run by its dispatcher thread, which holds no digest, pair or
+// queue lock): every chunk sits partly filled in an upload while `want` writers wait for one, so
+// holders that are not inside a call hand their partly filled chunks over (hashed like a full one,
+// then freed), oldest first, until `want` chunks are on their way.  One holder is locked at a time
+// (a locked holder cannot be freed, parked or settled meanwhile) and the scan stops there, so an
+// idle digest's next call waits for one hand-over at most, not for a walk over every open upload.
+// (A fused pair's unconfirmed leader Write waits in its scratch buffer, never in the chunk.)
+// Lock order: dreg.mu, then a holder by try_lock, then the queue's mutex inside the hand-over --
+// nothing takes dreg.mu while holding a queue's mutex.  Returns whether anything was handed over.
+bool reclaim_chunks(void* arg, uint32_t want) {
   efes_ctx* ctx = static_cast<efes_ctx*>(arg);
-  std::vector<OpenRef> got;
-  {
-    std::lock_guard<std::mutex> lk(ctx->dreg.mu);
-    got.reserve(ctx->dreg.open.size());
-    for (const OpenRef& r : ctx->dreg.open)
-      if (r.d ? r.d->mu.try_lock() : r.f->mu.try_lock()) got.push_back(r);
+  uint32_t got = 0;
+  std::lock_guard<std::mutex> lk(ctx->dreg.mu);
+  for (const OpenRef& r : ctx->dreg.open) {
+    if (got >= want) break;
+    std::mutex& m = r.d ? r.d->mu : r.f->mu;
+    if (!m.try_lock()) continue;
+    efes_upload* u = r.d ? r.d->u : r.f->u;
+    if (u && efes::upload_handover(u)) ++got;
+    m.unlock();
   }
-  // Locked holders cannot be freed, parked or settled meanwhile (each needs the lock we hold).
-  bool any = false;
-  for (const OpenRef& r : got) {
-    efes_upload* u = r.d ? r.d->u : (r.f->open && !r.f->scratch ? nullptr : r.f->u);
-    if (u && efes::upload_handover(u)) any = true;
-    if (r.d) r.d->mu.unlock();
-    else r.f->mu.unlock();
-  }
-  return any;
+  return got > 0;
 }
 
 // Evicts the oldest digest (or fused pair) of ctx's queue that is not inside a call, has been idle
@@ -653,17 +636,14 @@ void count_fused(size_t n) {
   k.fused_bytes.fetch_add(n, std::memory_order_relaxed);
 }
 
-enum class Bind { kNo, kDone, kPending };
+enum class Bind { kNo, kPending };
 
 // A parked SHA-1 digest's Write (p, n) joins the CRC digest whose last Write was the same (p, n)
-// (MultiWriter(f, CRC32, Sha1) just made it).  c.d is the SHA-1 digest (its mutex held), parked and
-// not fused.
-//   scratch mode: the CRC digest's Write is deferred in its scratch buffer.  The pair opens ONE
-//     upload keeping both hashes (SHA-1 from the SHA-1 digest's parked state, CRC from the CRC
-//     digest's) and the deferred bytes become the pair's open leader Write, which the SHA-1 Write
-//     then confirms as a follower (kPending: c.z and c.zk are set);
-//   other modes: the CRC digest's fresh upload holds exactly those bytes, staged and not handed
-//     over; they are compared here and the upload keeps both hashes from now on (kDone).
+// (MultiWriter(f, CRC32, Sha1) just made it) and is deferred in its scratch buffer.  c.d is the
+// SHA-1 digest (its mutex held), parked and not fused.  The pair opens ONE upload keeping both
+// hashes (SHA-1 from the SHA-1 digest's parked state, CRC from the CRC digest's) and the deferred
+// bytes become the pair's open leader Write, which the SHA-1 Write then confirms as a follower
+// (kPending: c.z and c.zk are set).
 Bind try_bind(Call& c, const uint8_t* p, size_t n) {
   Digest* f = c.d;
   Digest* l;
@@ -680,68 +660,41 @@ Bind try_bind(Call& c, const uint8_t* p, size_t n) {
     l->cand_p = nullptr;
   }
   std::unique_lock<std::mutex> llk(l->mu, std::adopt_lock);
-  if (l->fz || l->latched || l->sha()) return Bind::kNo;
-  if (l->defer) {
-    if (l->u || l->defer_n != n) return Bind::kNo;
-    efes_ctx* on = place(l);
-    if (!placed_on(f, on)) return Bind::kNo;
-    int rc = EFES_OK;
-    efes_queue* q = efes::stream_queue(on, &rc);
-    if (!q) return Bind::kNo;
-    bool no_slot = false;
-    efes_upload* u = nullptr;
-    if (efes::upload_open_slot(q, EFES_HASH_SHA1 | EFES_HASH_CRC32, &f->sbase, &l->cbase, &u, &no_slot) != EFES_OK)
-      return Bind::kNo;  // no free slot: both go on alone (l stages its Write at its next call)
-    Fused* z = new (std::nothrow) Fused;
-    if (!z) {
-      efes_upload_close(u);
-      return Bind::kNo;
-    }
-    // the pair is locked before an evictor or the reclaim hook can find it in the registry
-    c.zk = std::unique_lock<std::mutex>(z->mu);
-    c.z = z;
-    z->u = u;
-    z->on = on;
-    z->open = true;  // l's deferred Write is the pair's open leader Write
-    z->op = p;
-    z->on_bytes = n;
-    z->scratch = l->defer;
-    z->scratch_cap = l->defer_cap;
-    l->defer = nullptr;
-    z->last_ns.store(now_ns(), std::memory_order_relaxed);
-    {
-      std::lock_guard<std::mutex> lk(on->dreg.mu);
-      z->pos = on->dreg.open.insert(on->dreg.open.end(), OpenRef{nullptr, z});
-    }
-    l->fz = z;
-    f->fz = z;
-    counters().pairs.fetch_add(1, std::memory_order_relaxed);
-    return Bind::kPending;
-  }
-  if (!l->u || !placed_on(f, l->on)) return Bind::kNo;
-  efes_upload* u = l->u;
-  if (!efes::upload_holds_only(u, n)) return Bind::kNo;
-  if (memcmp(efes::upload_staged(u, 0), p, n) != 0) return Bind::kNo;  // the staged bytes ARE this Write
-  efes_sha1_state shadow = f->sbase;
-  if (efes::replay_write(&shadow, p, n) != EFES_OK) return Bind::kNo;  // Go panics: alone
+  if (l->fz || l->latched || l->sha() || !l->defer || l->u || l->defer_n != n) return Bind::kNo;
+  efes_ctx* on = place(l);
+  if (!placed_on(f, on)) return Bind::kNo;
+  int rc = EFES_OK;
+  efes_queue* q = efes::stream_queue(on, &rc);
+  if (!q) return Bind::kNo;
+  bool no_slot = false;
+  efes_upload* u = nullptr;
+  if (efes::upload_open_slot(q, EFES_HASH_SHA1 | EFES_HASH_CRC32, &f->sbase, &l->cbase, &u, &no_slot) != EFES_OK)
+    return Bind::kNo;  // no free slot: both go on alone (l stages its Write at its next call)
   Fused* z = new (std::nothrow) Fused;
-  if (!z) return Bind::kNo;
-  efes::upload_fuse(u, f->sbase, shadow);
+  if (!z) {
+    efes_upload_close(u);
+    return Bind::kNo;
+  }
+  // the pair is locked before an evictor or the reclaim hook can find it in the registry
+  c.zk = std::unique_lock<std::mutex>(z->mu);
+  c.z = z;
   z->u = u;
-  z->on = l->on;
-  z->pos = l->pos;
+  z->on = on;
+  z->open = true;  // l's deferred Write is the pair's open leader Write
+  z->op = p;
+  z->on_bytes = n;
+  z->scratch = l->defer;
+  z->scratch_cap = l->defer_cap;
+  l->defer = nullptr;
   z->last_ns.store(now_ns(), std::memory_order_relaxed);
   {
-    std::lock_guard<std::mutex> lk(l->on->dreg.mu);
-    *z->pos = OpenRef{nullptr, z};
+    std::lock_guard<std::mutex> lk(on->dreg.mu);
+    z->pos = on->dreg.open.insert(on->dreg.open.end(), OpenRef{nullptr, z});
   }
-  l->u = nullptr;
-  l->on = nullptr;
   l->fz = z;
   f->fz = z;
   counters().pairs.fetch_add(1, std::memory_order_relaxed);
-  count_fused(n);
-  return Bind::kDone;
+  return Bind::kPending;
 }
 
 // The leader's (CRC) Write in a live pair: it waits for the follower's.  False: the pair splits.
@@ -749,28 +702,16 @@ bool lead(Call& c, const uint8_t* p, size_t n) {
   Fused* z = c.z;
   if (n == 0) return true;    // crc32.go:76-86 of nothing
   if (z->open) return false;  // the follower never confirmed the previous one
-  const PairStage m = pair_stage();
-  if (m == PairStage::kScratch) {
-    size_t cap = 0;
-    uint8_t* b = scratch_get(n, &cap);
-    if (!b) return false;  // no memory for a scratch buffer
-    memcpy(b, p, n);
-    z->scratch = b;
-    z->scratch_cap = cap;
-    z->conf = 0;
-    z->open = true;
-    z->op = p;
-    z->on_bytes = n;
-    return true;
-  }
-  if (n > efes::upload_chunk_bytes(z->u)) return false;
-  uint64_t off = 0;
-  if (efes::upload_stage(z->u, p, n, &off, m == PairStage::kCached) == EFES_OK) {
-    z->open = true;
-    z->op = p;
-    z->on_bytes = n;
-    z->ooff = off;
-  }  // else the fault is latched in the upload
+  size_t cap = 0;
+  uint8_t* b = scratch_get(n, &cap);
+  if (!b) return false;  // no memory for a scratch buffer
+  memcpy(b, p, n);
+  z->scratch = b;
+  z->scratch_cap = cap;
+  z->conf = 0;
+  z->open = true;
+  z->op = p;
+  z->on_bytes = n;
   return true;
 }
 
@@ -786,13 +727,6 @@ bool follow(Call& c, const uint8_t*& p, size_t& n, efes_sha1_state* whole, bool*
   const efes_sha1_state s0 = efes::upload_shadow(u);
   efes_sha1_state sh = s0;
   if (efes::replay_write(&sh, p, n) != EFES_OK) return false;  // Go panics: alone
-  if (!z->scratch) {  // staged by the leader: compare
-    if (memcmp(pending(z), p, n) != 0) return false;
-    z->open = false;
-    (void)efes::upload_confirm(u, sh);  // a fault is latched in the upload for the sync points
-    count_fused(n);
-    return true;
-  }
   // Staged now, piece by piece (a Write larger than the room left in the chunk spans several), with
   // streaming stores compared with the leader's copy in the same pass.  Each piece is confirmed with
   // the Go state after it (its x[:nx] is what a later job continues from), the last one with the
@@ -841,16 +775,14 @@ int digest_write(Digest* d, const void* p0, size_t n0) {
     c.split();  // the Writes diverged: both continue alone
   }
   if (d->latched) return d->latched == EFES_ERR_STATE ? EFES_ERR_STATE : EFES_OK;
-  if (!split_mid && n > 0 && !d->u && fuse_enabled()) {
+  if (!split_mid && n > 0 && !d->u) {
     if (d->sha()) {
-      const Bind b = try_bind(c, p, n);
-      if (b == Bind::kDone) return EFES_OK;
-      if (b == Bind::kPending) {
+      if (try_bind(c, p, n) == Bind::kPending) {
         if (follow(c, p, n, &whole, &split_mid)) return EFES_OK;
         c.split();
         if (d->latched) return d->latched == EFES_ERR_STATE ? EFES_ERR_STATE : EFES_OK;
       }
-    } else if (pair_stage() == PairStage::kScratch) {
+    } else {
       // a CRC digest's first Write on a fresh upload waits for its MultiWriter partner
       size_t cap = 0;
       if (uint8_t* b = scratch_get(n, &cap)) {
@@ -863,16 +795,10 @@ int digest_write(Digest* d, const void* p0, size_t n0) {
       }
     }
   }
-  const bool fresh = !d->u;
   int rc = acquire(d);
   if (rc == EFES_OK) rc = efes_upload_write(d->u, p, n);
   if (rc == EFES_OK && split_mid) efes::upload_set_shadow(d->u, whole);  // Go made ONE Write of it
-  if (rc == EFES_OK) {
-    if (!d->sha() && fresh && n > 0 && fuse_enabled() && pair_stage() != PairStage::kScratch &&
-        efes::upload_holds_only(d->u, n))
-      candidate(d, p, n);
-    return EFES_OK;
-  }
+  if (rc == EFES_OK) return EFES_OK;
   d->latched = rc;
   return rc == EFES_ERR_STATE ? EFES_ERR_STATE : EFES_OK;
 }

@@ -373,10 +373,7 @@ uint32_t efes_crc32_combine(uint32_t crc1, uint32_t crc2, uint64_t len2);
 int efes_crc32_span(efes_ctx* ctx, const void* data_device, uint64_t length, efes_crc32_state* crc_device,
                     void* stream);
 
-/* Test hook (ABI 6): the k-th launch from now of ctx's digest queue (k = 0: none) reports a device
- * fault instead of running, as a faulted kernel would, and the queue stays faulted.  For the
- * fault-latching tests of the Go surface; an explicit call, so no environment can switch it on. */
-int efes_debug_fault_after(efes_ctx* ctx, uint64_t k);
+/* Test hooks are declared in efes_testing.h: exported, but not part of the stable surface. */
 
 /* Pure text codecs on plain states (no device work). */
 void efes_sha1_state_marshal_text(const efes_sha1_state* s, char out[200]);

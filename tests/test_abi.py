@@ -10,12 +10,21 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "efes_hash.h")
+HEADERS = [HEADER, os.path.join(ROOT, "include", "efes_testing.h")]
 
 
-def declared_functions():
-    src = open(HEADER).read()
-    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(efes_\w+)\s*\(", src)))
+def declared_functions(headers=HEADERS):
+    names = set()
+    for h in headers:
+        src = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
+        names |= set(re.findall(r"\b(efes_\w+)\s*\(", src))
+    return sorted(names)
+
+
+def test_test_hooks_are_outside_the_stable_header():
+    """efes_debug_fault_after is a test hook, declared in efes_testing.h only."""
+    assert "efes_debug_fault_after" not in declared_functions([HEADER])
+    assert declared_functions([HEADERS[1]]) == ["efes_debug_fault_after"]
 
 
 def test_every_declared_symbol_is_exported(efes_lib):
@@ -279,3 +288,124 @@ def test_integration_doc_two_build_targets():
     if os.path.isdir(ref):
         assert "CGO_ENABLED=0 go build" in open(os.path.join(ref, "Makefile")).read().split("\n")[5]
         assert "CGO_ENABLED=0" in open(os.path.join(ref, ".goreleaser.yml")).read().split("\n")[8]
+
+
+# ---- the Go binding of INTEGRATION.md (no Go toolchain here: its ownership rules, checked as text) --
+REF = "/root/reference"
+DIGEST_FILES = ("sha1.go", "sha1_efes.go", "crc32.go", "crc32_efes.go")  # replaced under -tags efesgpu
+
+
+def _go_blocks():
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    return re.findall(r"```go\n(.*?)```", doc, flags=re.S)
+
+
+def _go_funcs(src: str):
+    """(receiver, type, name, body) of every top-level func of a Go source text."""
+    out = []
+    for m in re.finditer(r"^func (?:\((\w+) \*?(\w+)\) )?(\w+)\(", src, flags=re.M):
+        i = src.index("{", m.end())
+        depth, j = 0, i
+        while True:
+            depth += {"{": 1, "}": -1}.get(src[j], 0)
+            if depth == 0:
+                break
+            j += 1
+        out.append((m.group(1), m.group(2), m.group(3), src[i:j + 1]))
+    return out
+
+
+def test_go_binding_never_copies_a_handle_holder():
+    """`*d = *newSha1Handle(true)` copied a handle out of a temporary whose
+    finalizer then freed it (a use-after-free on every resumed PATCH).  No Go block may assign
+    through a dereference to a struct value (`*x = *y`, `*x = T{...}`) or copy a digest value."""
+    for b in _go_blocks():
+        assert not re.search(r"^\s*\*\w+\s*=", b, flags=re.M), re.search(r"^\s*\*\w+\s*=.*$", b, flags=re.M)
+        assert not re.search(r"=\s*\*(?:d|w|\w+Handle\(|New\w+\()", b), "a dereferenced digest copied"
+
+
+def test_go_binding_finalizer_is_on_the_handle_owner():
+    """Every runtime.SetFinalizer target is the object whose handle field the same function
+    allocates (`&x.c` / `&x.u` passed to C), so the handle lives exactly as long as its owner."""
+    found = 0
+    for b in _go_blocks():
+        for recv, _typ, name, body in _go_funcs(b):
+            for target, fin in re.findall(r"runtime\.SetFinalizer\((\w+),\s*([^)]*\)?)\)", body):
+                if fin.strip() == "nil":
+                    continue
+                found += 1
+                assert re.search(rf"&{target}\.(c|u)\b", body), (name, target)
+                assert target == recv or re.search(rf"\b{target} := new\(\w+\)", body), (name, target)
+    assert found >= 3  # sha1digest, crc32digest, uploadWriter
+
+
+def test_go_binding_keeps_the_owner_alive_across_c_calls():
+    """Every method that hands its handle (`d.c` through handle(), `w.u`) to C calls
+    runtime.KeepAlive on the receiver after its last such call, so the finalizer cannot free the
+    handle while C uses it.  The finalizer itself (free) and the allocation (`&d.c`, before any
+    finalizer exists) are exempt."""
+    checked = 0
+    for b in _go_blocks():
+        for recv, typ, name, body in _go_funcs(b):
+            if not recv or name == "free":
+                continue
+            uses = [m.end() for m in re.finditer(rf"C\.efes_\w+\([^;\n]*(?<!&)\b{recv}\.(?:c|u|handle\(\))", body)]
+            if not uses:
+                continue
+            checked += 1
+            keep = [m.start() for m in re.finditer(rf"runtime\.KeepAlive\({recv}\)", body)]
+            assert keep and max(keep) > max(uses), f"{typ}.{name}: no runtime.KeepAlive({recv}) after its C call"
+    assert checked >= 15
+
+
+def test_go_binding_replaces_the_digest_files_whole():
+    """The -tags efesgpu file stands in for sha1.go, sha1_efes.go, crc32.go and crc32_efes.go (the
+    _efes.go files read Go struct fields and define MarshalText/UnmarshalText, so they cannot
+    compile beside it): every method the four define on sha1digest / crc32digest is defined by the
+    binding, no other reference file defines one, and every package-level name of the four that
+    another reference file uses is defined by the binding.  Needs the reference (skipped without)."""
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    for f in DIGEST_FILES:
+        assert f"`{f}`" in doc[doc.index("## 1. Build"):doc.index("## 3.")], f
+    if not os.path.isdir(REF):
+        pytest.skip("reference not present")
+    binding = next(b for b in _go_blocks() if "//go:build efesgpu" in b)
+    mine = {(t, n) for r, t, n, _ in _go_funcs(binding) if r}
+    mine_top = {n for r, _t, n, _ in _go_funcs(binding) if not r} | set(re.findall(r"^var (\w+)", binding, flags=re.M)) \
+        | set(re.findall(r"^type (\w+)", binding, flags=re.M))
+    theirs, defined = set(), set()
+    for f in DIGEST_FILES:
+        src = open(os.path.join(REF, f)).read()
+        theirs |= {(t, n) for r, t, n, _ in _go_funcs(src) if r}
+        defined |= {n for r, _t, n, _ in _go_funcs(src) if not r}
+        defined |= set(re.findall(r"^(?:var|const|type) (\w+)", src, flags=re.M))
+        for blk in re.findall(r"^(?:var|const) \((.*?)^\)", src, flags=re.M | re.S):
+            defined |= set(re.findall(r"^\s+(\w+)", blk, flags=re.M))
+    # the exported method sets (hash.Hash, encoding.TextMarshaler/TextUnmarshaler, Sum32); sha1.go's
+    # unexported checkSum is its own Sum's helper and no other file calls a digest's unexported method
+    assert {m for m in theirs if m[0] in ("sha1digest", "crc32digest") and m[1][0].isupper()} <= mine
+    for f in sorted(os.listdir(REF)):
+        if not f.endswith(".go") or f in DIGEST_FILES:
+            continue
+        src = open(os.path.join(REF, f)).read()
+        src = re.sub(r'//.*$|"(?:\\.|[^"\\])*"|`[^`]*`', "", src, flags=re.M)  # code only
+        others = {(t, n) for r, t, n, _ in _go_funcs(src) if r and t in ("sha1digest", "crc32digest")}
+        assert not others, (f, others)
+        used = {n for n in defined if re.search(rf"(?<![.\w]){n}\b", src)}
+        assert used <= mine_top, (f, used - mine_top)
+
+
+def test_library_env_vars_are_the_documented_four():
+    """the product library reads exactly the sizing variables of INTEGRATION.md
+    §3's table, and no source under efes_amd/csrc has an A/B build switch left."""
+    names = set()
+    for f in os.listdir(os.path.join(ROOT, "efes_amd", "csrc")):
+        src = open(os.path.join(ROOT, "efes_amd", "csrc", f)).read()
+        names |= set(re.findall(r'getenv\("(\w+)"\)', src))
+        defines = set(re.findall(r"^#\s*if(?:n?def)?\s+(\w+)", src, flags=re.M)) - {"EFES_CHECKED"}
+        assert not {d for d in defines if d.startswith("EFES_")}, (f, defines)
+    want = {"EFES_DIGEST_STAGING_MIB", "EFES_DIGEST_CHUNK_KIB", "EFES_DIGEST_SLOTS", "EFES_DIGEST_EVICT_MS"}
+    assert names == want, names
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    for n in want:
+        assert f"| `{n}` |" in doc, n

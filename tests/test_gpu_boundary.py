@@ -311,3 +311,44 @@ def test_pool_skips_a_faulted_context(gpu, oracle):
         pool.close()
         for c in ctxs:
             c.close()
+
+
+_PATIENCE_CHILD = r"""
+import sys, time, hashlib, zlib
+sys.path[:0] = [{root!r}]
+from efes_amd import hashing
+ctx = hashing.Context(0)
+data = bytes(range(256)) * 400  # 102 400 bytes
+a, b, c = hashing.Sha1Digest(ctx), hashing.Sha1Digest(ctx), hashing.Sha1Digest(ctx)
+a.write(data)  # a and b hold the queue's two upload slots (EFES_DIGEST_SLOTS=2) ...
+b.write(data[:5000])
+t0 = time.perf_counter()
+c.write(data)  # ... so c's Write must evict one of them, idle for a few microseconds (a SHA-1
+               # digest: a CRC digest's first Write would wait in a scratch buffer for its partner)
+waited = time.perf_counter() - t0
+assert a.sum() == hashlib.sha1(data).digest() and b.sum() == hashlib.sha1(data[:5000]).digest()
+assert c.sum() == hashlib.sha1(data).digest()
+print("waited %.4f" % waited)
+"""
+
+
+@pytest.mark.parametrize("patience_ms", ["0", "1500"])
+def test_evict_patience(gpu, patience_ms):
+    """EFES_DIGEST_EVICT_MS (read when the library is loaded, so in a child process): on a queue with
+    two upload slots (EFES_DIGEST_SLOTS=2, below its 16 chunks: no chunk reclaim), a third digest's
+    Write evicts a holder idle for the patience -- at once with 0, after ~1.5 s with 1500 (the holders
+    went idle just before it) -- and every digest still equals hashlib/zlib."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, EFES_DIGEST_EVICT_MS=patience_ms, EFES_DIGEST_SLOTS="2", EFES_DIGEST_STAGING_MIB="1")
+    r = subprocess.run([sys.executable, "-c", _PATIENCE_CHILD.format(root=root)], env=env, capture_output=True,
+                       text=True, timeout=110)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    waited = float(r.stdout.split("waited")[1])
+    if patience_ms == "0":
+        assert waited < 0.5, waited
+    else:
+        assert 1.3 < waited < 10, waited

@@ -5,7 +5,8 @@ buffer, MarshalText or Sum), checked here against the CPU oracle and hashlib/zli
   * every saved .info text of the resumed PATCHes equals the oracle's after the same Writes;
   * every final Sum equals hashlib/zlib of the object;
   * fused (default): each byte staged and hashed once, every PATCH's pair bound, nothing split;
-  * unfused (EFES_DIGEST_FUSE=0): the same texts and digests, each byte hashed twice.
+  * unfused (the SHA-1 digest written from an equal copy of each buffer, so the pair never binds):
+    the same texts and digests, each byte hashed twice.
 """
 import hashlib
 import json
@@ -32,8 +33,8 @@ def _xorshift(n: int) -> bytes:  # the bytes tools/bench_go_surface.cpp hashes
     return bytes(out)
 
 
-@pytest.mark.parametrize("fuse", ["1", "0"])
-def test_go_surface_harness_against_oracle(tmp_path, oracle, fuse):
+@pytest.mark.parametrize("writes", ["same", "copy"])
+def test_go_surface_harness_against_oracle(tmp_path, oracle, writes):
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
@@ -41,9 +42,8 @@ def test_go_surface_harness_against_oracle(tmp_path, oracle, fuse):
         pytest.fail(f"{EXE} not built (__graft_entry__.build())")
     size, write, patches, threads, uploads, k = (1 << 20) + 12345, 32 << 10, 5, 8, 96, 6
     texts = tmp_path / "texts.txt"
-    env = dict(os.environ, EFES_DIGEST_FUSE=fuse)
     r = subprocess.run([EXE, str(threads), str(uploads), str(size), str(write), str(k), str(patches), "64", "256",
-                        str(texts)], capture_output=True, text=True, timeout=110, env=env)
+                        str(texts), writes], capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stdout + r.stderr
     res = json.loads(r.stdout.strip().splitlines()[-1])
     assert res["errors"] == 0 and res["all_equal"], res
@@ -59,7 +59,7 @@ def test_go_surface_harness_against_oracle(tmp_path, oracle, fuse):
             crc.write(piece)
             sha.write(piece)
         assert lines[p] == f"{sha.marshal_text()} {crc.marshal_text()}", p
-    if fuse == "1":
+    if writes == "same":
         assert res["hashed_bytes_per_byte"] == 1.0 and res["fused_bytes_per_byte"] == 1.0, res
         assert res["pairs"] == uploads * patches and res["settles"] == 0, res
     else:

@@ -99,12 +99,12 @@ OPS = ["mw", "mw", "mw", "mw", "crc_only", "sha_only", "mutated", "other_len", "
 def _script(gpu, oracle, rng: random.Random, steps: int, ctx=None, pool=None, tag=""):
     """A random sequence of Go-surface calls on one object; every sync point compared with the oracle."""
     o = Obj(gpu, oracle, ctx, pool)
-    size = 400_000  # every Write stays inside: off < 230 000, n <= 165 536
+    size = 800_000  # every Write stays inside: off < 430 000, n <= 365 536
     buf = _buf(size, rng.randrange(1 << 30))
     for k in range(steps):
         op = rng.choice(OPS)
         n = rng.choice([1, 55, 64, 4096, 32768, 32768, 40000, 65536])
-        off = rng.randrange(0, size - 170_000)
+        off = rng.randrange(0, size - 370_000)
         t = f"{tag} step {k} {op} n={n}"
         if op == "mw":  # the MultiWriter pattern: CRC then SHA-1, same (p, n)
             o.crc_write(buf, off, n)
@@ -160,9 +160,9 @@ def _script(gpu, oracle, rng: random.Random, steps: int, ctx=None, pool=None, ta
             o.check_sums(True, t)
         elif op == "sum_crc_first":
             o.check_sums(False, t)
-        elif op == "big":  # larger than a 64 KiB staging chunk
-            o.crc_write(buf, off, 100_000 + n)
-            o.sha_write(buf, off, 100_000 + n)
+        elif op == "big":  # larger than the default 256 KiB staging chunk: staged chunk by chunk
+            o.crc_write(buf, off, 300_000 + n)
+            o.sha_write(buf, off, 300_000 + n)
         elif op == "mw_two_buffers":  # equal bytes, different addresses: never bound, still right
             b2 = (ctypes.c_uint8 * n)()
             ctypes.memmove(b2, ctypes.addressof(buf) + off, n)
@@ -312,14 +312,15 @@ print("ok", d)
 """
 
 
-@pytest.mark.parametrize("mode", ["cached", "stream"])
-def test_diverging_pairs_other_staging_modes(gpu, mode):
-    """The random scripts under the non-default EFES_PAIR_STAGE modes (read once per process, so in
-    a child process): the leader's Write staged in the upload with ordinary or streaming stores
-    instead of waiting in a scratch buffer.  Every text and digest equals the oracle's."""
+def test_diverging_pairs_64k_chunks(gpu):
+    """The random scripts with EFES_DIGEST_CHUNK_KIB=64 (read when a context's digest queue is made,
+    so in a child process): most Writes, not only "big", span staging chunks, so the follower stages
+    the leader's scratch copy piece by piece across chunk boundaries and the pairs split mid-Write.
+    Every text and digest equals the oracle's (the default 256 KiB chunk left the
+    chunk-spanning paths to chance)."""
     tests = os.path.dirname(os.path.abspath(__file__))
     code = _MODE_CHILD.format(root=os.path.dirname(tests), tests=tests)
-    r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, EFES_PAIR_STAGE=mode),
+    r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, EFES_DIGEST_CHUNK_KIB="64"),
                        capture_output=True, text=True, timeout=110)
     assert r.returncode == 0 and "ok" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])
 

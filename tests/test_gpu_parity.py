@@ -1008,7 +1008,7 @@ def test_group_joint_phase_mixed_lengths_and_states(env, oracle, lanes):
 
 @pytest.mark.parametrize("force", ["4:40x", "8:24", "16:10x,4:30", "32:6,8:20", "64:3x", "0:0", "16:1000",
                                    "64:2x,32:4"])
-def test_planned_batch_forced_parts(env, oracle, force, monkeypatch):
+def test_planned_batch_forced_parts(env, oracle, force):
     """efes_hash_submit_plan: parts on side streams + the caller's stream, concurrently, some
     of them exclusive (CU-reserving LDS) -- every job lands in exactly one launch."""
     from efes_amd.batch import MODE_PLAN
@@ -1018,9 +1018,8 @@ def test_planned_batch_forced_parts(env, oracle, force, monkeypatch):
     offsets = np.concatenate([[0], np.cumsum(lengths)[:-1]]).astype(np.uint64)
     host = oracle.fill_synthetic(int(lengths.sum()) + 8, 77)
     buf = device_buffer(env, host)
-    monkeypatch.setenv("EFES_PLAN_FORCE", force)
     b = env["DeviceBatch"](buf.data_ptr(), offsets, lengths, fresh=True, ctx=env["ctx"])
-    b.make_plan()
+    b.make_plan(force)
     assert sum(p[0] for p in b.plan.parts()) == n
     b.run(MODE_PLAN)
     assert (b.status_host() == 0).all()
@@ -1031,7 +1030,7 @@ def test_planned_batch_forced_parts(env, oracle, force, monkeypatch):
 
 
 @pytest.mark.parametrize("force", ["1:32x,2:48x,4:40x", "2:20x,64:3x,1:16x", "1:40x,2:40x,8:20x,0:60"])
-def test_planned_batch_four_parts_fed_on_torch_stream(env, oracle, force, monkeypatch):
+def test_planned_batch_four_parts_fed_on_torch_stream(env, oracle, force):
     """Plans of four parts with FED lanes (FED4 = 1, FED4E = 2) beside grouped / DEEP / WIDE parts,
     submitted on a non-null torch stream (so the caller's stream is neither the context's nor a
     part stream): every part runs on its own part stream, forked from and joined back into the
@@ -1044,11 +1043,10 @@ def test_planned_batch_four_parts_fed_on_torch_stream(env, oracle, force, monkey
     offsets = np.concatenate([[0], np.cumsum(lengths)[:-1]]).astype(np.uint64)
     host = oracle.fill_synthetic(int(lengths.sum()) + 8, 78)
     buf = device_buffer(env, host)
-    monkeypatch.setenv("EFES_PLAN_FORCE", force)
     s = torch.cuda.Stream()
     with torch.cuda.stream(s):
         b = env["DeviceBatch"](buf.data_ptr(), offsets, lengths, fresh=True, ctx=env["ctx"])
-        b.make_plan()
+        b.make_plan(force)
         assert b.plan.nparts == 4 and sum(p[0] for p in b.plan.parts()) == n
         assert b.stream() != 0 and b.stream() != env["ctx"].stream
         b.submit(MODE_PLAN)
@@ -1144,24 +1142,25 @@ def test_full_size_config1_sha1_only(env, mode_name):
 
 
 def test_full_size_mixed_config_plan_equals_wide(env):
-    """BASELINE configs[3] at full size (65 536 chunks of the eleven ChunkSize classes 64K..64M,
-    752 GiB aliasing an 8 GiB pool, seed 7 as bench.py): the planner's concurrent parts (grouped
-    DEEP on reserved CUs + WIDE) and an all-WIDE run agree on every digest; one chunk per class
-    (and the longest) matches hashlib/zlib."""
+    """BASELINE configs[3] at full size and in the bench's own geometry (efes_amd.chunksize.mixed_geometry:
+    65 536 chunks of the eleven ChunkSize classes 64K..64M, 752 GiB at seeded offsets of a 200 GiB
+    pool filled with seed 0xEFE5, as bench.py's mixed leg): the planner's concurrent parts and an
+    all-WIDE run agree on every digest, and at least 64 chunks match hashlib/zlib on their own bytes --
+    the first and last chunk of every size class, of every plan part, the chunks on both sides of
+    every part boundary, and seeded extras (12 independent checks were too few)."""
     from efes_amd.batch import MODE_PLAN
-    from efes_amd.chunksize import MIXED_CLASSES
+    from efes_amd.chunksize import MIXED_CLASSES, mixed_geometry
     torch = env["torch"]
-    pool = 8 << 30
+    torch.cuda.empty_cache()
+    pool = 200 << 30
     buf = torch.empty(pool, dtype=torch.uint8, device="cuda:0")
     env["ctx"].fill_synthetic(buf.data_ptr(), pool, 0xEFE5, torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
-    rng = np.random.default_rng(7)
-    sizes = np.asarray(MIXED_CLASSES, dtype=np.uint64)[rng.integers(0, len(MIXED_CLASSES), 65536)]
-    sizes = np.sort(sizes)[::-1].copy()
-    offs = (rng.integers(0, (pool - sizes.astype(np.int64)) // 256 + 1) * 256).astype(np.uint64)
+    sizes, offs = mixed_geometry(65536, pool, 7)
     b = env["DeviceBatch"](buf.data_ptr(), offs, sizes, fresh=True, ctx=env["ctx"])
     b.make_plan()
-    assert len(b.plan.parts()) >= 2  # a real multi-part plan
+    parts = b.plan.parts()
+    assert len(parts) >= 2  # a real multi-part plan
     b.run(MODE_PLAN)
     assert (b.status_host() == 0).all()
     plan_sha, plan_crc = b.sha1_hex(), b.crc_sum().copy()
@@ -1169,9 +1168,25 @@ def test_full_size_mixed_config_plan_equals_wide(env):
     b.run(env["efes"].MODE_WIDE)
     assert (b.status_host() == 0).all()
     assert b.sha1_hex() == plan_sha and (b.crc_sum() == plan_crc).all()
-    picks = [0] + [int(np.argmax(sizes == c)) for c in MIXED_CLASSES if (sizes == c).any()]
-    _spot_check(env, buf, offs, sizes, plan_sha, plan_crc, picks)
-    del buf
+    # the plan runs the jobs longest-first: sizes are already in that order (a stable sort)
+    order, _ = env["ctx"].plan(sizes)
+    assert (order == np.arange(65536)).all()
+    picks = set()
+    for c in MIXED_CLASSES:
+        idx = np.flatnonzero(sizes == c)
+        picks |= {int(idx[0]), int(idx[-1])}
+    start = 0
+    for jobs, _mode, _x in parts:
+        picks |= {start, start + jobs - 1}
+        if start:
+            picks |= {start - 1, start}
+        start += jobs
+    rng = np.random.default_rng(0xC3)
+    while len(picks) < 72:
+        picks.add(int(rng.integers(0, 65536)))
+    assert len(picks) >= 64
+    _spot_check(env, buf, offs, sizes, plan_sha, plan_crc, sorted(picks))
+    del buf, b
     torch.cuda.empty_cache()
 
 

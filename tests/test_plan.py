@@ -78,16 +78,30 @@ def test_empty_and_zero_lengths():
     ("0:3000", [(3000, MODE_WIDE, False)]),
     ("0:5x", [(5, MODE_WIDE, True), (2995, MODE_WIDE, False)]),
 ])
-def test_force_override(monkeypatch, force, expect):
-    monkeypatch.setenv("EFES_PLAN_FORCE", force)
-    _, plan = plan_batch([MiB] * 3000)
-    assert plan.parts() == expect
+def test_caller_built_plan(force, expect):
+    """efes_plan is a plain struct a caller may fill itself (efes_amd.batch.forced_plan builds one from
+    a spec; the GPU tests force every part shape through efes_hash_submit_plan with it).  Round 5
+    removed the library's EFES_PLAN_FORCE environment override: a deployment's environment can no
+    longer change which kernels hash production bytes."""
+    from efes_amd.batch import forced_plan
+
+    plan = forced_plan(3000, force)
+    assert plan.njobs == 3000 and plan.parts() == expect
 
 
-def test_force_override_rejects_too_many_parts(monkeypatch):
-    """A forced plan that would need a fourth part is ignored (the model's plan stands)."""
+def test_caller_built_plan_rejects_too_many_parts():
+    from efes_amd.batch import forced_plan
+
+    with pytest.raises(ValueError):
+        forced_plan(3000, "4:10,8:10,16:10,32:10")
+    with pytest.raises(ValueError):
+        forced_plan(3000, "3:10")
+
+
+def test_planner_ignores_the_removed_override(monkeypatch):
+    """The old EFES_PLAN_FORCE variable set in the environment changes nothing."""
     _, model = plan_batch([MiB] * 3000)
-    monkeypatch.setenv("EFES_PLAN_FORCE", "4:10,8:10,16:10,32:10")
+    monkeypatch.setenv("EFES_PLAN_FORCE", "8:100")
     _, plan = plan_batch([MiB] * 3000)
     assert plan.parts() == model.parts()
 

@@ -13,9 +13,12 @@
 // (each request has its own io.Copy buffer).  All uploads hash the same bytes with the same PATCH
 // boundaries, so every Sum and every saved text must equal the first upload's, which bench.py and
 // tests/test_gpu_go_surface.py check against hashlib/zlib and the oracle.  Prints one JSON line.
+// `writes` = same (default: MultiWriter, both digests get the same buffer, the library fuses the
+// pair) or copy (the SHA-1 digest gets an equal copy at another address: the pair never binds, the
+// two digests are two uploads -- round 3's behaviour, each byte staged and hashed twice).
 // Not part of the product library.
 //   tools/bench_go_surface <threads> <uploads> <upload_bytes> <write_bytes> [open_per_thread]
-//                          [patches] [chunk_kib] [staging_mib] [texts_out]
+//                          [patches] [chunk_kib] [staging_mib] [texts_out|-] [writes]
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -43,7 +46,8 @@ struct Expect {
 
 // One group of uploads through one PATCH: new digests, resume, MultiWriter Writes, sync point.
 // Returns the number of mismatches against `ex` (or records into it when `record`).
-int patch_group(efes_pool* pool, const uint8_t* buf, size_t from, size_t to, size_t W, int p, int patches,
+int patch_group(efes_pool* pool, const uint8_t* buf, const uint8_t* sha_buf, size_t from, size_t to, size_t W, int p,
+                int patches,
                 std::vector<std::string>& sha_state, std::vector<std::string>& crc_state, Expect& ex, bool record,
                 std::atomic<int>& errs) {
   const size_t K = sha_state.size();
@@ -59,7 +63,7 @@ int patch_group(efes_pool* pool, const uint8_t* buf, size_t from, size_t to, siz
   for (size_t a = from; a < to; a += W) {
     const size_t m = std::min(W, to - a);
     for (size_t i = 0; i < K; ++i)
-      if (efes_crc32_write(crc[i], buf + a, m) || efes_sha1_write(sha[i], buf + a, m)) ++errs;
+      if (efes_crc32_write(crc[i], buf + a, m) || efes_sha1_write(sha[i], sha_buf + a, m)) ++errs;
   }
   const bool last = p == patches - 1;
   for (size_t i = 0; i < K; ++i) {
@@ -108,7 +112,7 @@ int main(int argc, char** argv) {
   const int pinned_cpus = pin_to_cpu_quota();  // see cpu_quota.hpp
   if (argc < 5) {
     fprintf(stderr, "usage: %s threads uploads upload_bytes write_bytes [open_per_thread] [patches] [chunk_kib] "
-                    "[staging_mib] [texts_out]\n", argv[0]);
+                    "[staging_mib] [texts_out|-] [same|copy]\n", argv[0]);
     return 2;
   }
   const int T = atoi(argv[1]);
@@ -118,7 +122,8 @@ int main(int argc, char** argv) {
   const int P = argc > 6 ? std::max(1, atoi(argv[6])) : 1;
   const char* chunk_kib = argc > 7 ? argv[7] : "256";
   const char* staging_mib = argc > 8 ? argv[8] : "8192";
-  const char* texts_out = argc > 9 ? argv[9] : nullptr;
+  const char* texts_out = argc > 9 && strcmp(argv[9], "-") ? argv[9] : nullptr;
+  const bool copy_writes = argc > 10 && !strcmp(argv[10], "copy");
   if (T < 1 || U < 1 || S < 1 || W < 1 || K < 1) return 2;
   // The digest queue is created at the first digest Write: size it like bench_uploads' queue.
   setenv("EFES_DIGEST_CHUNK_KIB", chunk_kib, 0);
@@ -150,7 +155,8 @@ int main(int argc, char** argv) {
   ex.crc_text.resize(P);
   {
     std::vector<std::string> ss(1), cs(1);
-    for (int p = 0; p < P; ++p) patch_group(pool, src.data(), cut[p], cut[p + 1], W, p, P, ss, cs, ex, true, errs);
+    for (int p = 0; p < P; ++p)
+      patch_group(pool, src.data(), src.data(), cut[p], cut[p + 1], W, p, P, ss, cs, ex, true, errs);
     if (errs) {
       fprintf(stderr, "reference upload failed\n");
       return 1;
@@ -167,6 +173,8 @@ int main(int argc, char** argv) {
   for (int t = 0; t < T; ++t)
     th.emplace_back([&, t] {
       std::vector<uint8_t> buf(src);  // this request's own bytes (its own io.Copy buffers)
+      std::vector<uint8_t> buf2(copy_writes ? src : std::vector<uint8_t>());
+      const uint8_t* sha_buf = copy_writes ? buf2.data() : buf.data();
       std::vector<long> mine;
       for (long u = t; u < U; u += T) mine.push_back(u);
       std::vector<double> ms;
@@ -175,7 +183,7 @@ int main(int argc, char** argv) {
         std::vector<std::string> ss(n), cs(n);
         for (int p = 0; p < P; ++p) {
           const auto a = clk::now();
-          bad += patch_group(pool, buf.data(), cut[p], cut[p + 1], W, p, P, ss, cs, ex, false, errs);
+          bad += patch_group(pool, buf.data(), sha_buf, cut[p], cut[p + 1], W, p, P, ss, cs, ex, false, errs);
           ms.push_back(std::chrono::duration<double, std::milli>(clk::now() - a).count());
         }
       }
@@ -202,13 +210,13 @@ int main(int argc, char** argv) {
   const double bytes = (double)U * (double)S;
   printf("{\"workload\": \"go_surface\", \"pinned_cpus\": %d, \"threads\": %d, \"uploads\": %ld, \"upload_bytes\": %zu, "
          "\"write_bytes\": %zu, \"open_per_thread\": %d, \"patches\": %d, \"chunk_kib\": %s, \"staging_mib\": %s, "
-         "\"fuse\": %s, \"seconds\": %.4f, \"value\": %.3f, \"unit\": \"GiB/s\", "
+         "\"writes\": \"%s\", \"seconds\": %.4f, \"value\": %.3f, \"unit\": \"GiB/s\", "
          "\"launches\": %llu, \"jobs\": %llu, \"hashed_bytes_per_byte\": %.4f, "
          "\"pairs\": %llu, \"fused_bytes_per_byte\": %.4f, \"settles\": %llu, "
          "\"patch_group_ms\": {\"p50\": %.3f, \"p90\": %.3f, \"p99\": %.3f, \"n\": %zu}, "
          "\"sum_sha1_crc32\": \"%s\", \"all_equal\": %s, \"errors\": %d}\n",
          pinned_cpus, T, U, S, W, K, P, chunk_kib, staging_mib,
-         getenv("EFES_DIGEST_FUSE") && !strcmp(getenv("EFES_DIGEST_FUSE"), "0") ? "false" : "true", secs,
+         copy_writes ? "copy" : "same", secs,
          bytes / secs / (1u << 30), (unsigned long long)(q1.launches - q0.launches),
          (unsigned long long)(q1.jobs - q0.jobs), (double)(q1.bytes - q0.bytes) / bytes,
          (unsigned long long)(f1.pairs - f0.pairs), (double)(f1.fused_bytes - f0.fused_bytes) / bytes,

@@ -197,7 +197,7 @@ def cpu_baseline(batch, data, n_chunks: int, chunk: int, threads: int, do_crc: b
 
 
 def host_inclusive(ctx, data, n: int, chunk: int, do_crc: bool, segment: int, batch):
-    """The same chunks starting in pinned host memory: H2D copies overlapped with hashing."""
+    """The same chunks starting in pinned host memory: H2D copies overlapped with hashing (DESIGN_NOTES.md)."""
     from efes_amd._lib import EFES_HOST_ZERO_COPY
     from efes_amd.batch import HostBatch, PinnedHostBuffer
 
@@ -311,7 +311,7 @@ def patch_latency_leg():
         return json.loads(r.stdout.strip().splitlines()[-1])
 
     points = []
-    for k, rounds in ((1, 20), (16, 8), (256, 4)):
+    for k, rounds in ((1, 20), (16, 8), (64, 6), (128, 4), (192, 4), (256, 4)):
         g = run([os.path.join(ROOT, "tools", "bench_go_surface"), str(k), str(k * rounds), str(4 << 20), str(32 << 10),
                  "1", "1", "256", "1024"])
         c = run([os.path.join(ROOT, "oracle", "patch_cpu"), str(k), str(4 << 20), "3"])
@@ -319,9 +319,13 @@ def patch_latency_leg():
                        "cpu_patch_ms": c["patch_ms"], "cpu_GiB/s": c["value"], "cpu_threads_pinned": c["pinned_cpus"],
                        "digests_match": g["sum_sha1_crc32"] == want and g["all_equal"] and
                        c["sum_sha1_crc32"] == want and c["all_equal"]})
-    return {"patch_bytes": 4 << 20, "points": points,
+    over = next((p["uploads_in_flight"] for p in points if p["gpu_GiB/s"] > p["cpu_GiB/s"]), None)
+    cores = points[0]["cpu_threads_pinned"]
+    return {"patch_bytes": 4 << 20, "points": points, "gpu_overtakes_cpu_at_uploads": over, "cpu_cores": cores,
             "note": "GPU: unchanged Go surface, one PATCH per request thread; CPU: oracle port of the same hashing "
-                    "(kind port) on the quota's cores; latency = one PATCH's Writes + Sums; not `value`"}
+                    "(kind port) on the quota's cores; latency = one PATCH's Writes + Sums; the efesgpu server "
+                    "hashes faster than the pure-Go build from gpu_overtakes_cpu_at_uploads in flight on "
+                    "cpu_cores host cores (INTEGRATION.md §1); not `value`"}
 
 
 def receiver_leg():
@@ -538,7 +542,7 @@ def make_workload(args, rank: int, world: int, ctx, device: str, stream):
                                    "launches": len(batches)}
 
 
-# Instruction-issue ceilings: a wave64 integer VALU instruction holds its SIMD
+# Instruction-issue ceilings (DESIGN_NOTES.md §4-5): a wave64 integer VALU instruction holds its SIMD
 # for 4 cycles (SQ_INSTS_VALU == SQ_ACTIVE_INST_VALU quad-cycles in profiles/r01_pmc), and
 #   DEEP: one message per wave; its SHA-1 chain is 405 VALU per 64-B block (80 rounds x 5 + 5);
 #   WIDE: one message per lane; VALU per 64-B block per wave from SQ_INSTS_VALU of a configs[4]-sized
@@ -817,7 +821,7 @@ def ingest_spot_check(data, batches, config) -> bool:
 
 
 def concurrency_leg(args, ctx, device: str, stream):
-    """How the rate of 4 MiB chunks depends on how many are in flight: one AUTO
+    """How the rate of 4 MiB chunks depends on how many are in flight (DESIGN_NOTES.md §4): one AUTO
     launch per count (DEEP up to one chunk per SIMD, FED4 / FED4E up to 32 / 48 per CU, GROUP4,
     then WIDE) over distinct bytes: up to 16 384 chunks (64 GiB) whole, beyond that each chunk as
     four 1 MiB segment Writes with the states resident (as the configs[4] leg), since 4 MiB x 65 536
@@ -886,7 +890,7 @@ def mixed_leg(args, rank: int, world: int, ctx, device: str, stream):
             "chunks": config["chunks_per_gpu"], "bytes": total, "plan": parts,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 5), "kernel_ms": round(kernel_ms, 3)},
-            "clock": clock, "note": "makespan set by the 64 MiB chunks' SHA-1 chains (DESIGN.md §4 batch planner); not `value`"}
+            "clock": clock, "note": "makespan set by the 64 MiB chunks' SHA-1 chains (DESIGN_NOTES.md §4 batch planner); not `value`"}
 
 
 def span_crc_leg(args, ctx, device: str, stream, gib: int = 16, reps: int = 5):

@@ -244,7 +244,7 @@ int efes_ctx_device(const efes_ctx* ctx) { return ctx ? ctx->device : -1; }
 void* efes_ctx_stream(efes_ctx* ctx) { return ctx ? static_cast<void*>(ctx->stream) : nullptr; }
 
 int efes_auto_mode(const efes_ctx* ctx, uint32_t njobs) {
-  // The lowest per-job latency that fits in one pass: DEEP up to one job per
+  // The lowest per-job latency that fits in one pass (DESIGN_NOTES.md §4): DEEP up to one job per
   // SIMD (46.5 ms per 4 MiB job); FED4 up to 32 jobs per CU (48.5 ms: DEEP's chain, fed from
   // two producer SIMDs -- below GROUP32/16/8's 49/52/57 ms at 2/4/8 jobs per SIMD); FED4E up to
   // 48 per CU (55.5 ms); grouped DEEP G = 4 (67 ms, 64 jobs per CU) up to 16 jobs per SIMD, i.e.

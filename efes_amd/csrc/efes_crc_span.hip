@@ -21,7 +21,7 @@
 //     after its last line (one GF(2) product with lane_op[k] = x^(8*64*k)), the lanes are
 //     XOR-reduced, the sum is advanced over the bytes after the range (op[w], computed on the
 //     host) and XORed into the state with one atomic per workgroup.
-// Bound: HBM read (every byte once); measured at ~93 % of a pure read kernel (DESIGN.md §4 "Span
+// Bound: HBM read (every byte once); measured at ~93 % of a pure read kernel (DESIGN_NOTES.md §4 "Span
 // CRC").  No SHA-1, no MFMA.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -95,10 +95,10 @@ __global__ __launch_bounds__(64) void span_prep_kernel(const uint8_t* __restrict
 // at tt*128, copy c at c*4 -- so a lookup's address is ONE v_perm_b32 (byte 1 = the index byte,
 // byte 0 = 4c, byte 2 = r, byte 3 = 0) and the table's 128 goes in the ds_read offset.
 // (Measured and not kept: 16 copies in one 64 KiB region with two workgroups per CU -- 2-way
-// conflicts, 32 waves per CU -- ran at the same rate; DESIGN.md §4 "Span CRC".)
+// conflicts, 32 waves per CU -- ran at the same rate; DESIGN_NOTES.md §4 "Span CRC".)
 constexpr int kSpanCopies = 32;
 constexpr int kSpanWavesPerSimd = 4;  // one workgroup per CU
-// (The row shift keeps one copy: 2 or 4 copies measured no faster, DESIGN.md.)
+// (The row shift keeps one copy: 2 or 4 copies measured no faster, DESIGN_NOTES.md.)
 struct SpanLDS {
   uint32_t slice[2][256][2][kSpanCopies];  // 128 KiB at LDS address 0
   uint32_t row_shift[4][256];              // 4 KiB

@@ -8,7 +8,7 @@
 // EFES_ERR_STATE.  The tail buffer x is updated byte-for-byte as Go does, stale bytes
 // included, so MarshalText (sha1_efes.go:25-38) of a device state equals Go's.
 //
-// Two kernel shapes:
+// Two kernel shapes (DESIGN_NOTES.md):
 //   DEEP: one chain wavefront per job.  SHA-1 is a strict chain of 64-byte compressions, so a
 //         job's speed is one wave's issue rate.  A producer wave on the same SIMD loads 64
 //         consecutive blocks (4 KiB, coalesced), computes their CRC-32 partials (combined by a
@@ -176,7 +176,7 @@ struct DeepJob {
 // the same instructions, so the chain reads W+K straight from registers -- no LDS traffic.
 // The chaining value moves from lane off+i to lane off+i+1 by DPP wave_shr:1 (5 v_mov_dpp
 // per block).  Measured against W+K read back from LDS by ds_read_b128: 48.1 vs 52.7 ms per
-// 1024 x 4 MiB.
+// 1024 x 4 MiB (DESIGN_NOTES.md §4).
 template <bool kAligned16>
 __device__ void deep_bulk(const Tables& T, int lane, const uint8_t* q, uint64_t nbulk, bool do_sha, bool do_crc,
                           uint32_t (&h)[5], uint32_t& crc_raw) {
@@ -629,7 +629,7 @@ __device__ __forceinline__ uint32_t group_last(uint32_t v, int lane) {
 // (lane m*G+i runs block i of job m), so a super-step of 410 G + ~700 instructions advances
 // k jobs by G blocks each: (410 G + ~700)/64 instructions per block of issue work (DEEP: 422)
 // at a per-job latency of 410 + ~700/G per block (WIDE: 740 at a slower issue rate).
-// DESIGN.md §4 "grouped DEEP".
+// DESIGN_NOTES.md §4 "grouped DEEP".
 //
 // Phases per wave: the head of every job (sequential, state parked in LDS); joint rounds in
 // which the jobs with >= G bulk blocks left advance together; then, per job, the rest
@@ -1304,7 +1304,7 @@ __device__ __forceinline__ void wide_bulk(const uint8_t* q, uint64_t nbulk, uint
   // tools/microbench/mb_wide_fetch: profiles/r04_fetch/): the second half of a line was often
   // evicted from L2 before the lane came back for it.  A holds the even block, B / C the odd one.
   for (; b + 5 < nmin; b += 4) {
-    if (b % 8 == 0) wide_pace(prog, w, nw, (uint32_t)b);  // every 8 blocks
+    if (b % 32 == 0) wide_pace(prog, w, nw, (uint32_t)b);  // every 32 blocks (profiles/r05_wide_pace_ab/)
     const uint8_t* qb = q + 64 * b;
     wide_step<kSha, kCrc>(A, t, h, crc_raw, true);
     load_block_le<kAligned16>(qb + 128, A);

@@ -3,7 +3,7 @@
 //
 // SHA-1 is a chain per job (sha1.go:129-203 runs block after block), so a batch's makespan is
 // at least its longest job's latency, and the kernel shapes trade latency for issue work.
-// Per 64-B block, in SIMD cycles (MI355X, measured: DESIGN.md §4 "grouped DEEP"):
+// Per 64-B block, in SIMD cycles (MI355X, measured: DESIGN_NOTES.md §4 "grouped DEEP"):
 //   shape                      latency of one job           SIMD work per job
 //   DEEP  (one wave per job)   422 x 4.1                    422 x 4.1
 //   GROUPn (64/n jobs / wave)  (410 + o_n/n) x 4.1          (410 n + o_n)/64 x 4.1
@@ -63,7 +63,7 @@ constexpr double kClock = 2.36e9;   // Hz (GRBM_GUI_ACTIVE during DEEP), for est
 constexpr int kWideLanes = 0;       // "shape" id of WIDE in the search
 constexpr int kFed = 1;             // "shape" id of FED4 (EFES_MODE_FED4)
 constexpr int kFedE = 2;            // "shape" id of FED4E (EFES_MODE_FED4E)
-// jobs per CU and cycles of one 4-block chain super-step (tools/fed_stats.py, DESIGN.md §4 FED)
+// jobs per CU and cycles of one 4-block chain super-step (tools/fed_stats.py, DESIGN_NOTES.md §4 FED)
 constexpr double fed_jobs_per_cu(int g) { return g == kFed ? 32.0 : 48.0; }
 constexpr double fed_cycles_per_step(int g) { return g == kFed ? 7005.0 : 8219.0; }
 constexpr bool is_fed(int g) { return g == kFed || g == kFedE; }
@@ -361,7 +361,7 @@ int efes_hash_submit_plan(efes_ctx* ctx, const efes_job* jobs, const efes_plan* 
   // The part streams, created on the first multi-part plan (plan_mu held).  They must land on
   // distinct hardware queues, or parts meant to run side by side serialize (configs[3] in a fresh
   // process: 1.03-1.09 s per step on ordinary streams, 0.885 s on CU-masked streams, which get a
-  // queue each).  A driver that refuses CU masking still gets ordinary streams.
+  // queue each; DESIGN_NOTES.md §4).  A driver that refuses CU masking still gets ordinary streams.
   for (int i = 0; i < EFES_PLAN_MAX_PARTS; ++i)
     if (!ctx->side[i] && efes::own_queue_stream(ctx, &ctx->side[i]) != hipSuccess &&
         hipStreamCreateWithFlags(&ctx->side[i], hipStreamNonBlocking) != hipSuccess) {

@@ -218,7 +218,7 @@ void efes_queue::run() {
     lk.unlock();  // callers keep staging while this batch is copied and launched
     // No H2D copy of the data: the DEEP kernel reads the pinned chunks in place (4 KiB per
     // wave per super-step, prefetched a super-step ahead, so the PCIe latency is hidden behind
-    // the chain).  Measured 2.5x the rate of staging copies.
+    // the chain).  Measured 2.5x the rate of staging copies (DESIGN_NOTES.md).
     hipError_t e = hipSuccess;
     if (e == hipSuccess) e = hipMemcpyAsync(dj, hj, sizeof(efes_job) * b.items.size(), hipMemcpyHostToDevice, stream);
     // DEEP (or grouped DEEP beyond one chunk per SIMD): efes::pcie_mode.

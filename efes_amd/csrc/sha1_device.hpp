@@ -3,7 +3,7 @@
 // Restates the compression function `block` of /root/reference/sha1.go:129-203
 // (FIPS 180-4 SHA-1) in the shape that is cheapest to ISSUE on one CDNA4 wavefront:
 // a lone wave issues about one VALU instruction per ~4.5 cycles and a dependent
-// VALU op has ~8.5 cycles latency (measured, DESIGN.md "Measured constants"), so the
+// VALU op has ~8.5 cycles latency (measured, DESIGN_NOTES.md "Measured constants"), so the
 // per-message rate is set by the instruction count of the chain.  Each round is
 // exactly five VALU ops:
 //     z  = e + WK[i]                      v_add_u32   (W[i] + K pre-added off-chain)

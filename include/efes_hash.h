@@ -145,7 +145,7 @@ int efes_auto_mode(const efes_ctx* ctx, uint32_t njobs);
  * grouped-DEEP beside the rest, which run WIDE.
  * efes_plan_batch orders the jobs longest-first (order[i] = index into `lengths` of the job to
  * place at jobs_device[i]) and picks the cuts, shapes and exclusivity from an issue-time model
- * of the kernels calibrated on MI355X; efes_hash_submit_plan launches a batch
+ * of the kernels calibrated on MI355X (DESIGN_NOTES.md §4); efes_hash_submit_plan launches a batch
  * laid out in that order: each part on a part stream of its own (created one after the other, so
  * usually -- HIP assigns hardware queues round-robin over all streams of the process, so not
  * certainly -- on distinct hardware queues), after the work queued on `stream`, which then waits
@@ -299,9 +299,7 @@ typedef struct efes_crc32 efes_crc32;
  *     UnmarshalText / free of one, an eviction) splits the pair: every confirmed byte is in both
  *     states, an unconfirmed CRC Write in the CRC state only, and both go on alone.
  * Every digest therefore hashes exactly the bytes of its own Writes, in order, whatever the caller
- * does; only the speed depends on the pattern.  EFES_DIGEST_FUSE=0 (env) disables binding;
- * EFES_PAIR_STAGE=scratch|cached|stream (env) picks where a leader's Write waits.
- * Process-wide counters: */
+ * does; only the speed depends on the pattern.  Process-wide counters: */
 typedef struct efes_pair_stats {
     uint64_t pairs;         /* CRC + SHA-1 digests bound to one upload */
     uint64_t fused_writes;  /* SHA-1 Writes confirming the CRC Write (one staging copy, one job) */

@@ -1,5 +1,5 @@
 // Microbenchmark: per-wave issue rate and SHA-1 chain cost on gfx950.
-// Used once to pick the kernel shape (DESIGN.md "Measured constants"). Not part of the product.
+// Used once to pick the kernel shape (DESIGN_NOTES.md "Measured constants"). Not part of the product.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>

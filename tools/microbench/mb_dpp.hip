@@ -1,6 +1,6 @@
 // Microbenchmark: issue cost of the cross-lane moves the DEEP chain could hand its chaining value
 // on with (one wave per SIMD, 8 independent moves per step).  The chain uses 5 DPP wave_shr:1
-// moves per 64-B block; DESIGN.md's accounting puts them at ~7.6 cycles each.  Not part of the
+// moves per 64-B block; DESIGN_NOTES.md's accounting puts them at ~7.6 cycles each.  Not part of the
 // product.
 //   hipcc --offload-arch=gfx950 -O3 -o mb_dpp mb_dpp.hip && ./mb_dpp
 #include <hip/hip_runtime.h>

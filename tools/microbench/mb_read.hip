@@ -1,4 +1,4 @@
-// mb_read.hip -- the practical HBM read ceiling for the span CRC's access shapes (DESIGN.md §4 "Span CRC").
+// mb_read.hip -- the practical HBM read ceiling for the span CRC's access shapes (DESIGN_NOTES.md §4 "Span CRC").
 // Every byte of a 16 GiB buffer is read once with global_load_dwordx4 and XOR-folded (one store per
 // lane at the end), in the shapes the span kernel can use:
 //   coal : each wave-instruction reads 1 KiB contiguous (lane j: 16 B at 16 j)

@@ -1,5 +1,5 @@
 // mb_wide_fetch.hip -- calibrates rocprofv3's FETCH_SIZE for the WIDE kernel's access pattern
-// (DESIGN.md §4 "WIDE at full load").  MI355X_MICROARCH.md calibrates FETCH_SIZE
+// (DESIGN_NOTES.md §4 "WIDE at full load").  MI355X_MICROARCH.md calibrates FETCH_SIZE
 // only for wide coalesced streams (it reports exactly half of their bytes); WIDE instead reads, per
 // lane, its own message in 64-B blocks as four 16-B global_load_dwordx4 (one lane per message, so one
 // wave-instruction touches 64 distinct cache lines), two blocks ahead of the block being hashed.

@@ -4,7 +4,7 @@ Each of T threads reads its own in-memory "file" of S bytes through efes_amd.has
 32 KiB reads (one seek back and re-read half way, as a retried PATCH does), then Sums; the digests
 are checked against hashlib.  Prints per-stream and aggregate MB/s for T = 1, 16, 64, 256 next to
 the oracle's Sha1File (the C restatement of the Go path) on one host core.  One SHA-1 stream is a
-chain: on the GPU it advances at one wavefront's issue rate (DESIGN.md §5 "When the GPU path
+chain: on the GPU it advances at one wavefront's issue rate (DESIGN_NOTES.md §5 "When the GPU path
 pays"), so a single stream is slower than a host core and the GPU wins by concurrency.
     python tools/sha1file_rate.py [size_mib]
 """

@@ -1,4 +1,4 @@
-"""How much do WIDE's LDS bank conflicts cost?  (DESIGN.md §4 "WIDE at full load".)
+"""How much do WIDE's LDS bank conflicts cost?  (DESIGN_NOTES.md §4 "WIDE at full load".)
 
 WIDE's CRC-32 looks up pos[o][byte] for the 64 byte positions o of every block; for one position all
 lanes of a 32-lane group read the same 1 KiB table, so the bank is byte mod 32 and random bytes give

@@ -561,7 +561,8 @@ class ClockMeter:
     """The effective engine clock over a timed region (the VALU-issue ceilings scale with it), read two
     ways at once:
       probe -- two marker launches on the measured stream (tools/clockprobe.hip) bracket the region;
-               each records s_memtime (shader clock, per XCD) and s_memrealtime (100 MHz) per XCD;
+               each records s_memtime (shader clock) and s_memrealtime (100 MHz) per CU, matched by
+               CU (memtime counters of different units have different offsets), median over CUs;
       smi   -- amdsmi's per-XCD current_gfxclk, polled every 2 ms by a host thread, averaged.
     Calibrated against GRBM_GUI_ACTIVE / 8 / ns of the same kernels (profiles/r05_clock/).  Either
     may be missing (no probe library, no amdsmi): the leg then reports what it has."""
@@ -640,7 +641,7 @@ class ClockMeter:
             mhz, sec, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_int()
             if self.probe.clockprobe_read(self.dev, ctypes.byref(mhz), ctypes.byref(sec), ctypes.byref(n)) == 0:
                 out.update({"probe_mhz": round(mhz.value, 1), "probe_seconds": round(sec.value, 4),
-                            "probe_xcds": n.value})
+                            "probe_cus": n.value})
         if self._thread:
             self._stop = True
             self._thread.join()

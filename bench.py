@@ -547,10 +547,10 @@ def make_workload(args, rank: int, world: int, ctx, device: str, stream):
 #   DEEP: one message per wave; its SHA-1 chain is 405 VALU per 64-B block (80 rounds x 5 + 5);
 #   WIDE: one message per lane; VALU per 64-B block per wave from SQ_INSTS_VALU of a configs[4]-sized
 #         launch: WIDE_VALU_FUSED (SHA-1 rounds + schedule, 16 byte swaps, 97 CRC-32 ops from the
-#         position tables, loop; 715.0 with round 4's whole-line loads, profiles/r04_wide_lines/clock.log;
-#         716.5 in round 3, 725 with slicing-by-8) and WIDE_VALU_SHA1 (SHA-1 only: 613.8, profiles/r03_wide_pmc/sha1_only_summary.txt,
-#         1.23552e11 / (3 072 waves x 65 536 blocks)).
-WIDE_VALU_FUSED = 715.0
+#         position tables, loop; 712.4 with round 5's pacing every 32 blocks, profiles/r05_clock/clock2.txt;
+#         715.0 with round 4's whole-line loads, 716.5 in round 3, 725 with slicing-by-8) and WIDE_VALU_SHA1
+#         (SHA-1 only: 613.8, profiles/r03_wide_pmc/sha1_only_summary.txt, 1.23552e11 / (3 072 waves x 65 536 blocks)).
+WIDE_VALU_FUSED = 712.4
 WIDE_VALU_SHA1 = 613.8
 CLOCK_HZ = 2.4e9
 N_SIMD = 1024
@@ -564,8 +564,8 @@ class ClockMeter:
                each records s_memtime (shader clock) and s_memrealtime (100 MHz) per CU, matched by
                CU (memtime counters of different units have different offsets), median over CUs;
       smi   -- amdsmi's per-XCD current_gfxclk, polled every 2 ms by a host thread, averaged.
-    Calibrated against GRBM_GUI_ACTIVE / 8 / ns of the same kernels (profiles/r05_clock/).  Either
-    may be missing (no probe library, no amdsmi): the leg then reports what it has."""
+    Calibrated against GRBM_GUI_ACTIVE / 8 / ns of the same kernels (profiles/r05_clock/): `mhz` is
+    the probe's (within 1 %), the amdsmi mean only when the probe library is missing."""
 
     def __init__(self, dev_index: int):
         import ctypes
@@ -650,7 +650,9 @@ class ClockMeter:
                 s = sorted(self._samples)
                 out.update({"smi_mhz_mean": round(sum(s) / len(s), 1), "smi_mhz_min": round(s[0], 1),
                             "smi_mhz_max": round(s[-1], 1), "smi_samples": len(s)})
-        out["mhz"] = out.get("smi_mhz_mean", out.get("probe_mhz"))
+        # the probe: within 0.1-1 % of GRBM_GUI_ACTIVE in the same run; the amdsmi mean strays by up to
+        # 6 % (it samples clock transients between launches; profiles/r05_clock/calibration.txt)
+        out["mhz"] = out.get("probe_mhz", out.get("smi_mhz_mean"))
         return out
 
 

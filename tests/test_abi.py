@@ -409,3 +409,19 @@ def test_library_env_vars_are_the_documented_four():
     doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
     for n in want:
         assert f"| `{n}` |" in doc, n
+
+
+def test_integration_load_rule_and_gauges():
+    """INTEGRATION.md §1 states the in-flight load below which the GPU server build
+    hashes slower than the pure-Go build, from bench.py's patch_latency leg, and the gauges it names are
+    the ones the binding's collector registers; the collector never opens the GPUs itself."""
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    rule = doc[doc.index("**Load rule for `efes-server`.**"):doc.index("## 2.")]
+    assert "patch_latency" in rule and "8.5 × C uploads are in flight" in rule
+    binding = next(b for b in _go_blocks() if "//go:build efesgpu" in b)
+    registered = set(re.findall(r'prometheus\.NewDesc\("(efes_gpu_\w+)"', binding))
+    named = set(re.findall(r"`(efes_gpu_\w+)(?:\{gpu\})?`", rule))
+    assert named and named <= registered, (named, registered)
+    assert "prometheus.MustRegister(gpuCollector{})" in binding
+    collect = next(body for r, t, n, body in _go_funcs(binding) if n == "Collect")
+    assert "pool()" not in collect and "gpuReady.Load()" in collect

@@ -303,7 +303,7 @@ def _go_blocks():
 def _go_funcs(src: str):
     """(receiver, type, name, body) of every top-level func of a Go source text."""
     out = []
-    for m in re.finditer(r"^func (?:\((\w+) \*?(\w+)\) )?(\w+)\(", src, flags=re.M):
+    for m in re.finditer(r"^func (?:\((?:(\w+) )?\*?(\w+)\) )?(\w+)\(", src, flags=re.M):
         i = src.index("{", m.end())
         depth, j = 0, i
         while True:

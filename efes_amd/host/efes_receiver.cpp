@@ -675,13 +675,17 @@ const char* const kPhaseNames[kPhases] = {"create", "open", "reserve", "read", "
 // Charges the calling thread's CPU time (user + system) since the last mark to a phase (when
 // enabled): with hundreds of request threads on 16 cores, wall time per phase would mostly be
 // run-queue waits.
-// EFES_RECEIVER_PHASE_CLOCK=wall charges wall time instead (where a request WAITS: run queue,
-// locks, pacing, its GPU chain).
+// EnableSavePhases(on, wall_clock = true) charges wall time instead (where a request WAITS: run
+// queue, locks, pacing, its GPU chain).
 uint64_t phase_ns() {
   struct timespec ts;
   clock_gettime(g_phase_clock.load(std::memory_order_relaxed), &ts);
   return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
 }
+// saveFile's copy path: io.Copy's own buffer + efes_upload_write (default), or the body read straight
+// into the upload's pinned staging (efes_upload_reserve / commit).
+std::atomic<bool> g_copy_buffer{true};
+
 struct PhaseClock {
   bool on = g_phases_on.load(std::memory_order_relaxed);
   uint64_t t = on ? phase_ns() : 0;
@@ -694,12 +698,13 @@ struct PhaseClock {
 };
 }  // namespace
 
-void EnableSavePhases(bool on) {
-  const char* c = getenv("EFES_RECEIVER_PHASE_CLOCK");
-  g_phase_clock.store(c && !strcmp(c, "wall") ? CLOCK_MONOTONIC : CLOCK_THREAD_CPUTIME_ID, std::memory_order_relaxed);
+void EnableSavePhases(bool on, bool wall_clock) {
+  g_phase_clock.store(wall_clock ? CLOCK_MONOTONIC : CLOCK_THREAD_CPUTIME_ID, std::memory_order_relaxed);
   for (auto& v : g_phase_ns) v.store(0, std::memory_order_relaxed);
   g_phases_on.store(on, std::memory_order_relaxed);
 }
+void SetSaveFileCopyBuffer(bool on) { g_copy_buffer.store(on, std::memory_order_relaxed); }
+
 void SavePhaseTotals(uint64_t ns[kPhases]) {
   for (int p = 0; p < kPhases; ++p) ns[p] = g_phase_ns[p].load(std::memory_order_relaxed);
 }
@@ -757,11 +762,8 @@ Error saveFile(Hasher* h, const std::string& path, int64_t offset, int64_t lengt
   // request-thread CPU-s per GiB against 0.56-0.58 for reading the body straight into the pinned
   // staging (efes_upload_reserve/commit), whose cold lines cost a read-for-ownership each and
   // then serve the file write from farther away (profiles/r03_receiver/ab_copybuf.log).
-  // EFES_RECEIVER_COPYBUF=0 selects the reserve/commit path.
-  static const bool staged_copy = [] {
-    const char* e = getenv("EFES_RECEIVER_COPYBUF");
-    return !(e && *e == '0');
-  }();
+  // SetSaveFileCopyBuffer(false) selects the reserve/commit path.
+  const bool staged_copy = g_copy_buffer.load(std::memory_order_relaxed);
   if (staged_copy) {
     static thread_local uint8_t cbuf[kCopyBuf];
     for (;;) {

@@ -158,7 +158,7 @@ Error saveFile(Hasher* h, const std::string& path, int64_t offset, int64_t lengt
                int64_t* new_offset, bool* done, DigestSums* sums);
 std::string OffsetMismatchText(int64_t given, int64_t required);  // OffsetMismatchError.Error()
 
-// Host CPU accounting of saveFile by phase (tools/bench_receiver, EFES_RECEIVER_PHASES=1): the
+// Host CPU accounting of saveFile by phase (tools/bench_receiver, EnableSavePhases): the
 // request threads' CPU nanoseconds (CLOCK_THREAD_CPUTIME_ID) summed over every request, per
 // phase.  Off by default (one branch per phase); when on, one clock read and one relaxed atomic
 // add per phase.
@@ -174,7 +174,11 @@ enum SavePhase {
   kPhaseInfo,     // DeleteFileInfo / SaveFileInfo at the end
   kPhases
 };
-void EnableSavePhases(bool on);
+void EnableSavePhases(bool on, bool wall_clock = false);  // wall_clock: CLOCK_MONOTONIC instead
+// saveFile's body copy: io.Copy's 32 KiB buffer then efes_upload_write (true, the default and the
+// cheaper on the host), or the body read straight into the upload's pinned staging
+// (efes_upload_reserve / efes_upload_commit).  Process-wide; set it before serving requests.
+void SetSaveFileCopyBuffer(bool on);
 void SavePhaseTotals(uint64_t ns[kPhases]);
 const char* SavePhaseName(int p);
 

@@ -794,7 +794,7 @@ static void test_concurrent_uploads(const std::string& root, int threads, int up
 
 int main(int argc, char** argv) {
   if (argc < 3) {
-    fprintf(stderr, "usage: %s cpu|gpu <tmpdir> [threads] [uploads]\n", argv[0]);
+    fprintf(stderr, "usage: %s cpu|gpu <tmpdir> [threads] [uploads] [copybuf|reserve]\n", argv[0]);
     return 2;
   }
   const std::string mode = argv[1], root = argv[2];
@@ -809,6 +809,7 @@ int main(int argc, char** argv) {
   } else if (mode == "gpu") {
     const int threads = argc > 3 ? atoi(argv[3]) : 16;
     const int uploads = argc > 4 ? atoi(argv[4]) : 4;
+    if (argc > 5 && !strcmp(argv[5], "reserve")) SetSaveFileCopyBuffer(false);  // efes_upload_reserve/commit
     int rc = efes_ctx_create(0, &g_ctx);
     if (rc) {
       fprintf(stderr, "efes_ctx_create: %s\n", efes_strerror(rc));

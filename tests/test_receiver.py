@@ -32,13 +32,13 @@ def test_receiver_cpu(tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("copybuf", ["1", "0"], ids=["copybuf", "reserve_commit"])
+@pytest.mark.parametrize("copybuf", ["copybuf", "reserve"], ids=["copybuf", "reserve_commit"])
 def test_receiver_gpu(tmp_path, copybuf):
     """saveFile's two staging paths: io.Copy's buffer + efes_upload_write (default) and the body read
-    straight into the pinned staging (efes_upload_reserve/commit, EFES_RECEIVER_COPYBUF=0)."""
+    straight into the pinned staging (efes_upload_reserve/commit, SetSaveFileCopyBuffer(false))."""
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    r = _run(["gpu", str(tmp_path), "16", "4"], 110, {"EFES_RECEIVER_COPYBUF": copybuf})
+    r = _run(["gpu", str(tmp_path), "16", "4", copybuf], 110)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "receiver_test gpu ok" in r.stdout, r.stdout

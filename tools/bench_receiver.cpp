@@ -206,7 +206,8 @@ int main(int argc, char** argv) {
     }
     const char* ph = getenv("EFES_RECEIVER_PHASES");
     const bool phases = ph && *ph == '1';
-    EnableSavePhases(phases);
+    const char* pclk = getenv("EFES_RECEIVER_PHASE_CLOCK");  // this tool's switch, not the library's
+    EnableSavePhases(phases, pclk && !strcmp(pclk, "wall"));
     std::atomic<uint64_t> req_cpu_ns{0}, unlink_cpu_ns{0};
     double s0 = 0, s1 = 0;
     const double c0 = cpu_seconds(&s0);

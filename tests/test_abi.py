@@ -281,7 +281,7 @@ def test_integration_doc_two_build_targets():
     for role in ("`write`", "`drain`", "`server`"):
         assert role in sec, role
     # the reason, measured: one stream on the GPU vs one core
-    assert "0.084 GiB/s" in sec and "0.60 GiB/s" in sec
+    assert "0.085 GiB/s" in sec and "0.53–0.60 GiB/s" in sec
     assert "No binary routes between the two" in sec
     # the reference lines cited are the ones that build with CGO_ENABLED=0
     ref = "/root/reference"

@@ -88,61 +88,79 @@ __global__ __launch_bounds__(64) void span_prep_kernel(const uint8_t* __restrict
   *crc = ~gf2_mulmod(after_head_op, r) ^ tail;
 }
 
-// LDS: the four slicing-by-4 tables (crc32.go:138-149's slicing8Table[0..3]) with every entry
-// stored 32 times side by side, lane j reading copy j mod 32, so a ds_read_b32 serves each 32-lane
-// group in one LDS cycle with no bank conflict (random indices into one table conflict ~3.5-way).
-// Layout (bytes): region r (tables 2r, 2r+1) at r*64 KiB, entry e at e*256 within it, table 2r+tt
-// at tt*128, copy c at c*4 -- so a lookup's address is ONE v_perm_b32 (byte 1 = the index byte,
-// byte 0 = 4c, byte 2 = r, byte 3 = 0) and the table's 128 goes in the ds_read offset.
-// (Measured and not kept: 16 copies in one 64 KiB region with two workgroups per CU -- 2-way
-// conflicts, 32 waves per CU -- ran at the same rate; DESIGN_NOTES.md §4 "Span CRC".)
-constexpr int kSpanCopies = 32;
+// LDS: the four slicing-by-4 tables (crc32.go:138-149's slicing8Table[0..3]) in one 64 KiB block --
+// entry e of table t, copy c at byte e*256 + 64t + 4c, so table t sits in banks 16t..16t+15 -- and
+// the read ring.  Lane j reads copy j mod 16, and its four lookups per word visit the tables in the
+// rotated order t = (i + j/16) mod 4: in each lookup instruction the four 16-lane groups of a wave
+// read four different tables, 64 different banks, so no instruction conflicts.  (Rounds 2-4 had
+// every lane read the same table, which took 32 copies and 128 KiB for the same property.)  A
+// lookup's address is still ONE v_perm_b32: byte 1 = the index byte of x, byte 0 = 64t + 4c from
+// a lane constant, bytes 2-3 = 0.
+constexpr int kSpanCopies = 16;
 constexpr int kSpanWavesPerSimd = 4;  // one workgroup per CU
+constexpr int kSpanWaves = kSpanLanes / 64;
+constexpr int kLineWords = kSpanLine / 4;
+static_assert(kSpanLine == 64, "one ring slot = 64 lines of 4 x 16 bytes");
 // (The row shift keeps one copy: 2 or 4 copies measured no faster, DESIGN_NOTES.md.)
 struct SpanLDS {
-  uint32_t slice[2][256][2][kSpanCopies];  // 128 KiB at LDS address 0
-  uint32_t row_shift[4][256];              // 4 KiB
-  uint32_t wave_sum[kSpanLanes / 64];
+  uint32_t slice[256][4][kSpanCopies];  // 64 KiB at LDS address 0
+  // Wave v's slot holds its 64 lines of the current row, piece-major: piece k (bytes 16k..16k+15)
+  // of lane l's line at word 256k + 4l, so the 16-byte reads of a piece are contiguous over the
+  // wave (no bank conflict) and the LDS-DMA of piece k is one instruction.
+  uint32_t ring[kSpanWaves][64 * kLineWords];  // 64 KiB
+  uint32_t row_shift[4][256];                   // 4 KiB
+  uint32_t wave_sum[kSpanWaves];
 };
 
-constexpr int kLineWords = kSpanLine / 4;
-constexpr int kSpanBuf = 2;  // lines in flight per lane (round 2 A/B, profiles/r02_span/)
-
+// The lane's line read straight into registers (the partial last row only).
 __device__ __forceinline__ void load_line(const uint8_t* src, uint32_t (&w)[kLineWords]) {
   typedef uint32_t v4u __attribute__((ext_vector_type(4)));
   const __attribute__((address_space(1))) v4u* s = (const __attribute__((address_space(1))) v4u*)src;
 #pragma unroll
   for (int q = 0; q < kLineWords / 4; ++q) {
-    const v4u v = s[q];  // (a nontemporal load measured no faster, round 2)
+    const v4u v = s[q];
     w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
   }
 }
 
-// v_perm_b32 selector: byte 0 <- lane byte 0 (4c), byte 1 <- x byte k, byte 2 <- lane byte 2 (r),
-// byte 3 <- 0x00 (selector 12).  Selectors 0-3 pick the second operand's bytes, 4-7 the first's.
-constexpr uint32_t perm_sel(int k) { return 0x0C020000u | ((4u + (uint32_t)k) << 8); }
-
-__device__ __forceinline__ uint32_t lds_word(const SpanLDS& L, uint32_t byte_addr, uint32_t off) {
-  return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(&L.slice) + byte_addr + off);
+// The wave's 64 lines of one row into its ring slot by LDS-DMA with the nontemporal policy:
+// instruction k moves piece k of every lane's line (lane l's 16 bytes land at slot + 1024k + 16l).
+// The streamed bytes are read once, so they bypass the caches' retention (round 5: LDS-DMA nt
+// reads at 7.0-7.2 TB/s where register loads top out at 6.2-6.3, profiles/r05_span_nt/).  Issued
+// from inline assembly so the compiler does not see an LDS write in flight: it would otherwise
+// wait for the DMA before every table lookup (the slot is only read after the explicit wait in
+// span_kernel).  The lgkmcnt wait orders the slot's previous reads before the overwrite; M0 is the
+// slot's LDS byte address (one wait state between writing M0 and the DMA; M0 is a reserved register
+// the compiler does not take as a clobber).
+constexpr bool kCoalescedFetch = true;
+__device__ __forceinline__ void fetch_row(const uint8_t* line, uint32_t lane, uint32_t slot) {
+#pragma unroll
+  for (int k = 0; k < kLineWords / 4; ++k)
+    asm volatile(
+        "s_waitcnt lgkmcnt(0)\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off nt"
+        :
+        : "v"(kCoalescedFetch ? line - 48 * lane + 1024 * k : line + 16 * k), "s"(slot + 1024u * k)
+        : "memory");  // (M0 has no other user in span_kernel: checked in the ISA)
 }
-constexpr uint32_t kOff0 = 0, kOff1 = 128, kOff2 = 0, kOff3 = 128;  // table offsets within their region
 
-// Raw CRC (from a zero register) of one line: slicing-by-4 (the 4-byte form of crc32.go:157-161),
-// the lookups into this lane's copy.  l0 / l1: the lane's address bytes for region 0 / 1.
-__device__ __forceinline__ uint32_t line_raw(const SpanLDS& L, uint32_t l0, uint32_t l1,
+// Raw CRC (from a zero register) of one line: slicing-by-4 (the 4-byte form of crc32.go:157-161).
+// lb: byte i = the lane's 64t + 4c for its i-th lookup; sel[i]: the v_perm selector for it (byte 0
+// <- lb byte i, byte 1 <- x byte 3 - t, bytes 2-3 <- 0x00; selectors 0-3 pick the second operand's
+// bytes, 4-7 the first's, 12 a zero).
+__device__ __forceinline__ uint32_t line_raw(const SpanLDS& L, uint32_t lb, const uint32_t (&sel)[4],
                                              const uint32_t (&w)[kLineWords]) {
+  const char* base = reinterpret_cast<const char*>(&L.slice);
+  auto look = [&](uint32_t x, int i) {
+    return *reinterpret_cast<const uint32_t*>(base + __builtin_amdgcn_perm(x, lb, sel[i]));
+  };
   uint32_t x = w[0], crc = 0;  // x = crc ^ the next word (crc32.go:157's crc ^= ...)
 #pragma unroll
   for (int s = 0; s < kLineWords; ++s) {
-    const uint32_t t0 = lds_word(L, __builtin_amdgcn_perm(x, l0, perm_sel(3)), kOff0);  // tab[0][x >> 24]
-    const uint32_t t1 = lds_word(L, __builtin_amdgcn_perm(x, l0, perm_sel(2)), kOff1);  // tab[1][x >> 16 & 0xff]
-    const uint32_t t2 = lds_word(L, __builtin_amdgcn_perm(x, l1, perm_sel(1)), kOff2);  // tab[2][x >> 8 & 0xff]
-    const uint32_t t3 = lds_word(L, __builtin_amdgcn_perm(x, l1, perm_sel(0)), kOff3);  // tab[3][x & 0xff]
-    const uint32_t p = __builtin_amdgcn_bitop3_b32(t0, t1, t2, 0x96);
+    const uint32_t p = __builtin_amdgcn_bitop3_b32(look(x, 0), look(x, 1), look(x, 2), 0x96);
     if (s + 1 < kLineWords)
-      x = __builtin_amdgcn_bitop3_b32(p, t3, w[s + 1], 0x96);  // 6 VALU per 4 bytes
+      x = __builtin_amdgcn_bitop3_b32(p, look(x, 3), w[s + 1], 0x96);  // 6 VALU per 4 bytes
     else
-      crc = p ^ t3;
+      crc = p ^ look(x, 3);
   }
   return crc;
 }
@@ -157,15 +175,15 @@ __global__ __launch_bounds__(kSpanLanes, kSpanWavesPerSimd) void span_kernel(con
   {  // tables into LDS: each slicing entry kSpanCopies times (4 per ds_write_b128), the row shift once
     uint4* dst = reinterpret_cast<uint4*>(&L.slice);
     for (uint32_t i = threadIdx.x; i < sizeof(L.slice) / 16; i += kSpanLanes) {
-      const uint32_t word = 4 * i;  // region word >> 14, entry (word >> 6) & 255, table pair bit 5
-      const uint32_t v = a.tabs->slice8[2 * (word >> 14) + ((word >> 5) & 1u)][(word >> 6) & 255u];
+      const uint32_t word = 4 * i;  // entry word >> 6, table (word >> 4) & 3
+      const uint32_t v = a.tabs->slice8[(word >> 4) & 3u][word >> 6];
       dst[i] = make_uint4(v, v, v, v);
     }
     const uint4* s2 = reinterpret_cast<const uint4*>(a.span->row_shift);
     uint4* d2 = reinterpret_cast<uint4*>(L.row_shift);
     for (uint32_t i = threadIdx.x; i < sizeof(L.row_shift) / 16; i += kSpanLanes) d2[i] = s2[i];
   }
-  const uint32_t w = blockIdx.x, j = threadIdx.x;
+  const uint32_t w = blockIdx.x, j = threadIdx.x, wave = j / 64, lane = j % 64;
   const uint64_t q = a.nline / a.groups, r = a.nline % a.groups;
   const uint64_t count = q + (w < r ? 1 : 0);
   const uint64_t start = w < r ? w * (q + 1) : r * (q + 1) + (w - r) * q;
@@ -173,40 +191,38 @@ __global__ __launch_bounds__(kSpanLanes, kSpanWavesPerSimd) void span_kernel(con
   const uint32_t extra = (uint32_t)(count % kSpanLanes);  // lanes j < extra take one more line
   const uint8_t* p = a.bulk + (start + j) * kSpanLine;
   constexpr uint64_t kRow = (uint64_t)kSpanLine * kSpanLanes;
-  const uint32_t l0 = 4u * (j % kSpanCopies), l1 = l0 | (1u << 16);  // address bytes of regions 0 / 1
+  uint32_t lb = 0, sel[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t t = (uint32_t)(i + (int)(j / 16)) & 3u;
+    lb |= (64u * t + 4u * (j % kSpanCopies)) << (8 * i);
+    sel[i] = 0x0C0C0000u | ((4u + 3u - t) << 8) | (uint32_t)i;
+  }
+  const uint32_t slot = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)&L.ring[wave][0]);
   __syncthreads();
 
   uint32_t acc = 0;
   if (rows) {
-    // kSpanBuf lines in flight per lane: buffer k holds row g*kSpanBuf + k.  The loop body is
-    // branch-free so the compiler's vmcnt waits stay exact (a conditional load made it wait for
-    // every line): reloads past the last row re-read the last row (clamped address, never
-    // committed), and the rows % kSpanBuf left over are already in buffers 0.. after the loop.
-    // Scheduling barriers keep "chain of buffer k, reload buffer k" in order: left to itself the
-    // compiler interleaves the chains and waits for all lines before issuing any reload.
-    uint32_t buf[kSpanBuf][kLineWords];
-    const uint64_t groups_of_rows = rows / kSpanBuf, last = rows - 1;
+    // One row in flight per wave: the DMA of row g+1 lands while row g is hashed from registers.
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    const v4u* mine = reinterpret_cast<const v4u*>(&L.ring[wave][0]) + (kCoalescedFetch ? 4 * lane : lane);
+    fetch_row(p, lane, slot);
+    for (uint64_t g = 0; g < rows; ++g) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's row g is in its slot
+      uint32_t line[kLineWords];
 #pragma unroll
-    for (int k = 0; k < kSpanBuf; ++k) load_line(p + ((uint64_t)k < last ? k : last) * kRow, buf[k]);
-    for (uint64_t g = 0; g < groups_of_rows; ++g) {
-#pragma unroll
-      for (int k = 0; k < kSpanBuf; ++k) {
-        const uint32_t rk = line_raw(L, l0, l1, buf[k]);
-        __builtin_amdgcn_sched_barrier(0);
-        const uint64_t nxt = (g + 1) * kSpanBuf + k;
-        load_line(p + (nxt < last ? nxt : last) * kRow, buf[k]);
-        __builtin_amdgcn_sched_barrier(0);
-        acc = row_advance(L.row_shift, acc) ^ rk;
+      for (int k = 0; k < kLineWords / 4; ++k) {
+        const v4u v = mine[kCoalescedFetch ? k : 64 * k];
+        line[4 * k] = v.x; line[4 * k + 1] = v.y; line[4 * k + 2] = v.z; line[4 * k + 3] = v.w;
       }
+      if (g + 1 < rows) fetch_row(p + (g + 1) * kRow, lane, slot);
+      acc = row_advance(L.row_shift, acc) ^ line_raw(L, lb, sel, line);
     }
-#pragma unroll
-    for (int k = 0; k < kSpanBuf - 1; ++k)
-      if ((uint64_t)k < rows % kSpanBuf) acc = row_advance(L.row_shift, acc) ^ line_raw(L, l0, l1, buf[k]);
   }
   if (j < extra) {  // the partial last row
     uint32_t E[kLineWords];
     load_line(p + rows * kRow, E);
-    acc = row_advance(L.row_shift, acc) ^ line_raw(L, l0, l1, E);
+    acc = row_advance(L.row_shift, acc) ^ line_raw(L, lb, sel, E);
   }
   // Lane j's last line is followed, within the range, by (extra - 1 - j) mod L lines.
   const uint32_t after = (extra + kSpanLanes - 1 - j) % kSpanLanes;

@@ -114,7 +114,7 @@ __global__ __launch_bounds__(1024) void reg_kernel16(const uint8_t* __restrict__
 // ring.  W waves per workgroup (one workgroup per CU), each with R slots of CH bytes (CH / 1024
 // wave-instructions per chunk); COPY: the lane's piece is copied out to registers right after it
 // lands and the slot refilled at once (the load overlaps the compute on the registers).
-template <int W, int R, int CH, bool COPY>
+template <int W, int R, int CH, bool COPY, bool ST = false, int AUX = 2>
 __global__ __launch_bounds__(64 * W) void ring_kernel(const uint8_t* __restrict__ src, uint64_t chunks_total,
                                                       uint32_t* __restrict__ out) {
   constexpr int Q = CH / 1024;  // wave-instructions per chunk
@@ -128,8 +128,9 @@ __global__ __launch_bounds__(64 * W) void ring_kernel(const uint8_t* __restrict_
     const uint8_t* c = src + (first + (uint64_t)W * i + wave) * CH;
 #pragma unroll
     for (int q = 0; q < Q; ++q)
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(c + 1024 * q + 16 * lane),
-                                       (__attribute__((address_space(3))) void*)(&ring[wave][slot][64 * q]), 16, 0, 2);
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(ST ? c + 64 * lane + 16 * q : c + 1024 * q + 16 * lane),
+          (__attribute__((address_space(3))) void*)(&ring[wave][slot][64 * q]), 16, 0, AUX);
   };
   for (int s = 0; s < R; ++s)
     if ((uint64_t)s < n) issue(s, s);
@@ -153,16 +154,16 @@ __global__ __launch_bounds__(64 * W) void ring_kernel(const uint8_t* __restrict_
   out[(uint64_t)blockIdx.x * blockDim.x + threadIdx.x] = acc.x ^ acc.y ^ acc.z ^ acc.w ^ tables[(threadIdx.x * 7) & 16383];
 }
 
-template <int W, int R, int CH, bool COPY>
+template <int W, int R, int CH, bool COPY, bool ST = false, int AUX = 2>
 static double run_ring(const uint8_t* d, uint64_t bytes, uint32_t* out) {
   const int wgs = 256;
   const uint64_t chunks = bytes / CH / (uint64_t)(wgs * W) * (uint64_t)(wgs * W);
   hipEvent_t a, b;
   CHECK(hipEventCreate(&a));
   CHECK(hipEventCreate(&b));
-  hipLaunchKernelGGL((ring_kernel<W, R, CH, COPY>), dim3(wgs), dim3(64 * W), 0, 0, d, chunks, out);
+  hipLaunchKernelGGL((ring_kernel<W, R, CH, COPY, ST, AUX>), dim3(wgs), dim3(64 * W), 0, 0, d, chunks, out);
   CHECK(hipEventRecord(a, 0));
-  for (int i = 0; i < 5; ++i) hipLaunchKernelGGL((ring_kernel<W, R, CH, COPY>), dim3(wgs), dim3(64 * W), 0, 0, d, chunks, out);
+  for (int i = 0; i < 5; ++i) hipLaunchKernelGGL((ring_kernel<W, R, CH, COPY, ST, AUX>), dim3(wgs), dim3(64 * W), 0, 0, d, chunks, out);
   CHECK(hipEventRecord(b, 0));
   CHECK(hipEventSynchronize(b));
   float ms = 0;
@@ -235,6 +236,9 @@ int main(int argc, char** argv) {
   printf("ring nt, 64 KiB of tables beside it, one workgroup per CU:\n");
   printf("  16 waves x 1 x 4 KiB: %.2f  copy-out %.2f TB/s\n", run_ring<16, 1, 4096, false>(d, bytes, out),
          run_ring<16, 1, 4096, true>(d, bytes, out));
+  printf("  16 waves x 1 x 4 KiB, strided fetch (lane: 16 B of its own line): nt %.2f  plain %.2f TB/s\n",
+         run_ring<16, 1, 4096, true, true, 2>(d, bytes, out), run_ring<16, 1, 4096, true, true, 0>(d, bytes, out));
+  printf("  16 waves x 1 x 4 KiB, coalesced, plain: %.2f TB/s\n", run_ring<16, 1, 4096, true, false, 0>(d, bytes, out));
   printf("  16 waves x 2 x 2 KiB: %.2f  copy-out %.2f TB/s\n", run_ring<16, 2, 2048, false>(d, bytes, out),
          run_ring<16, 2, 2048, true>(d, bytes, out));
   printf("  8 waves x 2 x 4 KiB: %.2f  copy-out %.2f TB/s\n", run_ring<8, 2, 4096, false>(d, bytes, out),

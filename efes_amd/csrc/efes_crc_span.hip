@@ -14,15 +14,17 @@
 //     < 64 rest bytes byte-wise (crc32.go:125); the state becomes ~Z^m(~crc_head) ^ raw(rest)
 //     with m the bytes after the head -- every bulk contribution below is then XORed into it;
 //   * span_kernel: workgroup w owns a contiguous range of 64-byte lines; lane j takes lines j,
-//     j+L, j+2L, ... (a wave reads 4 KiB per row), computes each line's raw CRC by slicing-by-4
-//     from lane-private copies of the tables in LDS (no bank conflicts, one v_perm per lookup
-//     address) and folds it into its accumulator, acc = Z^(64L)(acc) ^ raw(line) (a byte-sliced
-//     4 x 256 table).  At the end, lane j's accumulator is advanced over the lines of the range
-//     after its last line (one GF(2) product with lane_op[k] = x^(8*64*k)), the lanes are
-//     XOR-reduced, the sum is advanced over the bytes after the range (op[w], computed on the
+//     j+L, j+2L, ... (a wave's 64 lines of a row are 4 KiB, staged into the wave's LDS slot by
+//     nontemporal LDS-DMA while the previous row is hashed), computes each line's raw CRC by
+//     slicing-by-4 from lane-private copies of the tables in LDS (no bank conflicts, one v_perm
+//     per lookup address) and folds it into its accumulator, acc = Z^(64L)(acc) ^ raw(line) (a
+//     byte-sliced 4 x 256 table).  At the end, lane j's accumulator is advanced over the lines of
+//     the range after its last line (one GF(2) product with lane_op[k] = x^(8*64*k)), the lanes
+//     are XOR-reduced, the sum is advanced over the bytes after the range (op[w], computed on the
 //     host) and XORed into the state with one atomic per workgroup.
-// Bound: HBM read (every byte once); measured at ~93 % of a pure read kernel (DESIGN_NOTES.md §4 "Span
-// CRC").  No SHA-1, no MFMA.
+// Bound: HBM read (every byte once).  Round 5: 6.61-6.62 TB/s against 7.0-7.2 for LDS-DMA nt reads
+// alone, with the engine clock power-limited to ~1.6 GHz while it runs (profiles/r05_span_ring/).
+// No SHA-1, no MFMA.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -104,9 +106,7 @@ static_assert(kSpanLine == 64, "one ring slot = 64 lines of 4 x 16 bytes");
 // (The row shift keeps one copy: 2 or 4 copies measured no faster, DESIGN_NOTES.md.)
 struct SpanLDS {
   uint32_t slice[256][4][kSpanCopies];  // 64 KiB at LDS address 0
-  // Wave v's slot holds its 64 lines of the current row, piece-major: piece k (bytes 16k..16k+15)
-  // of lane l's line at word 256k + 4l, so the 16-byte reads of a piece are contiguous over the
-  // wave (no bank conflict) and the LDS-DMA of piece k is one instruction.
+  // Wave v's slot holds its 64 lines of the current row, the pieces of each line rotated (fetch_row).
   uint32_t ring[kSpanWaves][64 * kLineWords];  // 64 KiB
   uint32_t row_shift[4][256];                   // 4 KiB
   uint32_t wave_sum[kSpanWaves];
@@ -123,8 +123,14 @@ __device__ __forceinline__ void load_line(const uint8_t* src, uint32_t (&w)[kLin
   }
 }
 
-// The wave's 64 lines of one row into its ring slot by LDS-DMA with the nontemporal policy:
-// instruction k moves piece k of every lane's line (lane l's 16 bytes land at slot + 1024k + 16l).
+// The wave's 64 lines of one row (4 KiB) into its ring slot by LDS-DMA with the nontemporal policy.
+// Instruction k moves the row's bytes 1024k..1024k+1023 (lines 16k..16k+15, coalesced) and lane l
+// of it lands at slot + 1024k + 16l.  Which 16 bytes lane l fetches is the swizzle (below): within
+// each 64-byte line the four pieces are rotated by (line / 4) mod 4, so that when every lane then
+// reads piece m of its own line, 16 neighbouring lanes hit 16 different 16-byte bank groups (the
+// plain layout, a 64-byte stride, conflicts 4-way).  Fetching piece-major instead (instruction k =
+// piece k of every line) avoids the conflict too but scatters each instruction over 4 KiB, which
+// reads at 3.7 TB/s with the nontemporal policy (profiles/r05_span_ring/).
 // The streamed bytes are read once, so they bypass the caches' retention (round 5: LDS-DMA nt
 // reads at 7.0-7.2 TB/s where register loads top out at 6.2-6.3, profiles/r05_span_nt/).  Issued
 // from inline assembly so the compiler does not see an LDS write in flight: it would otherwise
@@ -132,14 +138,21 @@ __device__ __forceinline__ void load_line(const uint8_t* src, uint32_t (&w)[kLin
 // span_kernel).  The lgkmcnt wait orders the slot's previous reads before the overwrite; M0 is the
 // slot's LDS byte address (one wait state between writing M0 and the DMA; M0 is a reserved register
 // the compiler does not take as a clobber).
-constexpr bool kCoalescedFetch = true;
-__device__ __forceinline__ void fetch_row(const uint8_t* line, uint32_t lane, uint32_t slot) {
+//   slot unit (16 B) u = 4*line + ((piece + line/4) mod 4)
+//   lane l of instruction k: unit 64k + l -> line 16k + l/4, piece ((l mod 4) - l/16) mod 4
+__device__ __forceinline__ uint32_t fetch_offset(uint32_t lane) {
+  return 64u * (lane >> 2) + 16u * (((lane & 3u) - (lane >> 4)) & 3u);
+}
+__device__ __forceinline__ uint32_t read_offset(uint32_t lane, int m) {
+  return 64u * lane + 16u * (((uint32_t)m + (lane >> 2)) & 3u);
+}
+__device__ __forceinline__ void fetch_row(const uint8_t* src, uint32_t slot) {  // src: row chunk + fetch_offset
 #pragma unroll
   for (int k = 0; k < kLineWords / 4; ++k)
     asm volatile(
         "s_waitcnt lgkmcnt(0)\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off nt"
         :
-        : "v"(kCoalescedFetch ? line - 48 * lane + 1024 * k : line + 16 * k), "s"(slot + 1024u * k)
+        : "v"(src + 1024 * k), "s"(slot + 1024u * k)
         : "memory");  // (M0 has no other user in span_kernel: checked in the ISA)
 }
 
@@ -205,17 +218,18 @@ __global__ __launch_bounds__(kSpanLanes, kSpanWavesPerSimd) void span_kernel(con
   if (rows) {
     // One row in flight per wave: the DMA of row g+1 lands while row g is hashed from registers.
     typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-    const v4u* mine = reinterpret_cast<const v4u*>(&L.ring[wave][0]) + (kCoalescedFetch ? 4 * lane : lane);
-    fetch_row(p, lane, slot);
+    const char* mine = reinterpret_cast<const char*>(&L.ring[wave][0]);
+    const uint8_t* src = p - kSpanLine * lane + fetch_offset(lane);
+    fetch_row(src, slot);
     for (uint64_t g = 0; g < rows; ++g) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's row g is in its slot
       uint32_t line[kLineWords];
 #pragma unroll
       for (int k = 0; k < kLineWords / 4; ++k) {
-        const v4u v = mine[kCoalescedFetch ? k : 64 * k];
+        const v4u v = *reinterpret_cast<const v4u*>(mine + read_offset(lane, k));
         line[4 * k] = v.x; line[4 * k + 1] = v.y; line[4 * k + 2] = v.z; line[4 * k + 3] = v.w;
       }
-      if (g + 1 < rows) fetch_row(p + (g + 1) * kRow, lane, slot);
+      if (g + 1 < rows) fetch_row(src + (g + 1) * kRow, slot);
       acc = row_advance(L.row_shift, acc) ^ line_raw(L, lb, sel, line);
     }
   }

@@ -16,6 +16,12 @@ fi
 timeout -k 10 300 python3 -u -m pytest tests/test_gpu_span.py -x -v --timeout 120 --timeout-method thread \
   > "$O/span_tests.log" 2>&1 || { tail -30 "$O/span_tests.log"; exit 1; }
 tail -3 "$O/span_tests.log"
+for lib in "${VARIANTS[@]}"; do  # every variant must be bit-exact before it is timed
+  timeout -k 10 300 env EFES_LIB_OVERRIDE="$PWD/efes_amd/lib/ab/libefeshash_$lib.so" python3 -u -m pytest \
+    tests/test_gpu_span.py -x -q --timeout 120 --timeout-method thread > "$O/span_tests_$lib.log" 2>&1 \
+    || { tail -30 "$O/span_tests_$lib.log"; exit 1; }
+  echo "$lib: $(tail -1 "$O/span_tests_$lib.log")"
+done
 B="--no-cpu-baseline --host-inclusive off --sha1-leg off --uploads-leg off --go-surface-leg off --latency-leg off --receiver-leg off --drain-leg off --concurrency-leg off --mixed-leg off --ingest-leg off --steps 2 --warmup 1"
 for rep in 1 2; do
   for lib in product "${VARIANTS[@]}"; do

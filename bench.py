@@ -941,7 +941,11 @@ def span_crc_leg(args, ctx, device: str, stream, gib: int = 16, reps: int = 5):
     return {"workload": f"one {gib} GiB object, CRC-32 only (efes_crc32_span)", "bytes": n,
             "value": round(n / (ms * 1e-3) / GiB, 1), "unit": "GiB/s", "kernel": "span_kernel",
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBPS, 4), "ms_per_call": round(ms, 3)},
+                         "frac": round(achieved / HBM_PEAK_GBPS, 4), "ms_per_call": round(ms, 3),
+                         "traffic": load_traffic("span_kernel", f"{gib}GiB:span"),
+                         "read_ceiling": {"value": 7100.0, "unit": "GB/s",
+                                          "source": "LDS-DMA nontemporal reads alone, 7.0-7.2 TB/s "
+                                                    "(tools/microbench/mb_glds, profiles/r05_span_nt/)"}},
             "cpu_port_1core": {"value": round((1 << 30) / cpu_s / GiB, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
                                "sample": "oracle crc32digest.Write (slicing-by-8, crc32.go:153-169) over the first GiB"},
             "crc_matches_zlib": ok, "clock": clock, "note": "HIP events on the launch stream; not `value`"}

@@ -13,7 +13,7 @@ timeout -k 10 400 env EFES_LIB_OVERRIDE="$V" python3 -u -m pytest tests/test_gpu
 tail -1 "$O/tests.log"
 B="--no-cpu-baseline --host-inclusive off --sha1-leg off --uploads-leg off --go-surface-leg off --latency-leg off \
  --receiver-leg off --drain-leg off --concurrency-leg off --mixed-leg off --ingest-leg off --span-leg off --steps 20 --warmup 3"
-for rep in 1 2; do
+for rep in ${REPS:-1 2}; do
   for lib in product $VAR; do
     env_lib=""; [ $lib = product ] || env_lib="EFES_LIB_OVERRIDE=$V"
     timeout -k 10 200 env $env_lib python3 bench.py $B > "$O/$lib.$rep.json" 2> "$O/$lib.$rep.err" || { tail -5 "$O/$lib.$rep.err"; exit 1; }

@@ -105,10 +105,10 @@ constexpr int kLineWords = kSpanLine / 4;
 static_assert(kSpanLine == 64, "one ring slot = 64 lines of 4 x 16 bytes");
 // (The row shift keeps one copy: 2 or 4 copies measured no faster, DESIGN_NOTES.md.)
 struct SpanLDS {
-  uint32_t slice[256][4][kSpanCopies];  // 64 KiB at LDS address 0
+  uint32_t row_shift[4][256];           // 4 KiB at LDS address 0 (a lookup: one SDWA shift, the table in the offset)
+  uint32_t slice[256][4][kSpanCopies];  // 64 KiB at 4 KiB (the ds_read offset)
   // Wave v's slot holds its 64 lines of the current row, the pieces of each line rotated (fetch_row).
   uint32_t ring[kSpanWaves][64 * kLineWords];  // 64 KiB
-  uint32_t row_shift[4][256];                   // 4 KiB
   uint32_t wave_sum[kSpanWaves];
 };
 
@@ -178,9 +178,10 @@ __device__ __forceinline__ uint32_t line_raw(const SpanLDS& L, uint32_t lb, cons
   return crc;
 }
 
-__device__ __forceinline__ uint32_t row_advance(const uint32_t (&s)[4][256], uint32_t v) {
-  return __builtin_amdgcn_bitop3_b32(s[0][v & 0xffu], s[1][(v >> 8) & 0xffu], s[2][(v >> 16) & 0xffu], 0x96) ^
-         s[3][v >> 24];
+// Z^(64L)(v) ^ raw: the row shift of v (four lookups) folded with the next line's raw CRC.
+__device__ __forceinline__ uint32_t row_advance(const uint32_t (&s)[4][256], uint32_t v, uint32_t raw) {
+  const uint32_t p = __builtin_amdgcn_bitop3_b32(s[0][v & 0xffu], s[1][(v >> 8) & 0xffu], s[2][(v >> 16) & 0xffu], 0x96);
+  return __builtin_amdgcn_bitop3_b32(p, s[3][v >> 24], raw, 0x96);
 }
 
 __global__ __launch_bounds__(kSpanLanes, kSpanWavesPerSimd) void span_kernel(const SpanArgs a) {
@@ -230,13 +231,13 @@ __global__ __launch_bounds__(kSpanLanes, kSpanWavesPerSimd) void span_kernel(con
         line[4 * k] = v.x; line[4 * k + 1] = v.y; line[4 * k + 2] = v.z; line[4 * k + 3] = v.w;
       }
       if (g + 1 < rows) fetch_row(src + (g + 1) * kRow, slot);
-      acc = row_advance(L.row_shift, acc) ^ line_raw(L, lb, sel, line);
+      acc = row_advance(L.row_shift, acc, line_raw(L, lb, sel, line));
     }
   }
   if (j < extra) {  // the partial last row
     uint32_t E[kLineWords];
     load_line(p + rows * kRow, E);
-    acc = row_advance(L.row_shift, acc) ^ line_raw(L, lb, sel, E);
+    acc = row_advance(L.row_shift, acc, line_raw(L, lb, sel, E));
   }
   // Lane j's last line is followed, within the range, by (extra - 1 - j) mod L lines.
   const uint32_t after = (extra + kSpanLanes - 1 - j) % kSpanLanes;

@@ -13,17 +13,21 @@
 //   * span_prep_kernel (one lane): the <= 15 head bytes up to the first 16-byte boundary and the
 //     < 64 rest bytes byte-wise (crc32.go:125); the state becomes ~Z^m(~crc_head) ^ raw(rest)
 //     with m the bytes after the head -- every bulk contribution below is then XORed into it;
-//   * span_kernel: workgroup w owns a contiguous range of 64-byte lines; lane j takes lines j,
-//     j+L, j+2L, ... (a wave's 64 lines of a row are 4 KiB, staged into the wave's LDS slot by
-//     nontemporal LDS-DMA while the previous row is hashed), computes each line's raw CRC by
-//     slicing-by-4 from lane-private copies of the tables in LDS (no bank conflicts, one v_perm
-//     per lookup address) and folds it into its accumulator, acc = Z^(64L)(acc) ^ raw(line) (a
-//     byte-sliced 4 x 256 table).  At the end, lane j's accumulator is advanced over the lines of
-//     the range after its last line (one GF(2) product with lane_op[k] = x^(8*64*k)), the lanes
-//     are XOR-reduced, the sum is advanced over the bytes after the range (op[w], computed on the
-//     host) and XORed into the state with one atomic per workgroup.
-// Bound: HBM read (every byte once).  Round 5: 6.61-6.62 TB/s against 7.0-7.2 for LDS-DMA nt reads
-// alone, with the engine clock power-limited to ~1.6 GHz while it runs (profiles/r05_span_ring/).
+//   * span_kernel: rows of L = 1024 lines (64 KiB) are dealt round-robin -- workgroup w takes rows
+//     w, w+G, w+2G, ... (G workgroups, one per CU), so the whole GPU sweeps the buffer front to back
+//     -- and lane j takes line j of each of its rows (a wave's 64 lines of a row are 4 KiB, staged
+//     into the wave's LDS slot by nontemporal LDS-DMA while the previous row is hashed).  Each
+//     line's raw CRC comes from slicing-by-4 on lane-private copies of the tables in LDS (no bank
+//     conflicts, one v_perm per lookup address) and is folded into the lane's accumulator,
+//     acc = Z^(64LG)(acc) ^ raw(line) (a byte-sliced 4 x 256 table the workgroup builds from the
+//     launch's stride operator).  At the end, lane j's accumulator is advanced over what follows
+//     its last line -- the rest of that row (lane_op[L-1-j]) and everything after the row (op[w],
+//     computed on the host), or for the partial last row lane_op[extra-1-j] and the rest bytes --
+//     the lanes are XOR-reduced and the sum XORed into the state with one atomic per workgroup.
+// Bound: HBM read (every byte once).  Round 5: 6.6-6.7 TB/s against 7.0-7.2 for LDS-DMA nt reads
+// alone, with the engine clock power-limited to ~1.6 GHz while it runs (profiles/r05_span_ring/);
+// sweeping rows round-robin rather than one contiguous range per workgroup keeps 6.3 TB/s on
+// buffers whose allocation left the per-range layout at 5.9 (profiles/r05_span_alloc/).
 // No SHA-1, no MFMA.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -58,9 +62,6 @@ static uint32_t xpow8n(uint64_t n) {
 }
 
 void build_span_tables(SpanTables* t) {
-  const uint32_t row = xpow8n((uint64_t)kSpanLine * kSpanLanes);  // one workgroup row: L lines
-  for (int b = 0; b < 4; ++b)
-    for (uint32_t v = 0; v < 256; ++v) t->row_shift[b][v] = gf2_mulmod(row, v << (8 * b));
   for (int k = 0; k < kSpanLanes; ++k) t->lane_op[k] = xpow8n((uint64_t)kSpanLine * (uint64_t)k);
 }
 
@@ -71,8 +72,10 @@ struct SpanArgs {
   const SpanTables* span;
   uint64_t nline;
   uint32_t groups;
+  uint32_t stride_op;           // x^(8 * 64 * L * groups): one workgroup's step from row to row
+  uint32_t rest_op;             // x^(8 * rest)
   uint32_t _pad;
-  uint32_t op[kSpanMaxGroups];  // x^(8 * bytes after workgroup w's range) mod P
+  uint32_t op[kSpanMaxGroups];  // x^(8 * bytes after workgroup w's last full row's line L-1) mod P
 };
 static_assert(sizeof(SpanArgs) <= 4096, "kernel argument segment");
 static_assert(kSpanLine % 4 == 0, "whole words per line");
@@ -193,18 +196,20 @@ __global__ __launch_bounds__(kSpanLanes, kSpanWavesPerSimd) void span_kernel(con
       const uint32_t v = a.tabs->slice8[(word >> 4) & 3u][word >> 6];
       dst[i] = make_uint4(v, v, v, v);
     }
-    const uint4* s2 = reinterpret_cast<const uint4*>(a.span->row_shift);
-    uint4* d2 = reinterpret_cast<uint4*>(L.row_shift);
-    for (uint32_t i = threadIdx.x; i < sizeof(L.row_shift) / 16; i += kSpanLanes) d2[i] = s2[i];
+    // the row shift for this launch's stride (groups rows): entry v of byte b = stride_op * (v << 8b)
+    L.row_shift[threadIdx.x >> 8][threadIdx.x & 255u] = gf2_mulmod(a.stride_op, (threadIdx.x & 255u) << (8 * (threadIdx.x >> 8)));
   }
+  // Rows of L lines are dealt round-robin: workgroup w takes rows w, w + G, w + 2G, ... (G =
+  // groups), so the whole GPU sweeps the buffer front to back; the partial last row (extra lines)
+  // goes to its round-robin owner.
   const uint32_t w = blockIdx.x, j = threadIdx.x, wave = j / 64, lane = j % 64;
-  const uint64_t q = a.nline / a.groups, r = a.nline % a.groups;
-  const uint64_t count = q + (w < r ? 1 : 0);
-  const uint64_t start = w < r ? w * (q + 1) : r * (q + 1) + (w - r) * q;
-  const uint64_t rows = count / kSpanLanes;               // rows every lane takes part in
-  const uint32_t extra = (uint32_t)(count % kSpanLanes);  // lanes j < extra take one more line
-  const uint8_t* p = a.bulk + (start + j) * kSpanLine;
+  const uint64_t G = a.groups, rtot = a.nline / kSpanLanes;
+  const uint32_t extra = (uint32_t)(a.nline % kSpanLanes);
+  const uint64_t rows = rtot > w ? (rtot - 1 - w) / G + 1 : 0;  // full rows of this workgroup
+  const bool partial = (rtot % G) == w && j < extra;            // this lane's line of the partial row
+  const uint8_t* p = a.bulk + ((uint64_t)w * kSpanLanes + j) * kSpanLine;
   constexpr uint64_t kRow = (uint64_t)kSpanLine * kSpanLanes;
+  const uint64_t kStride = kRow * G;
   uint32_t lb = 0, sel[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -230,18 +235,19 @@ __global__ __launch_bounds__(kSpanLanes, kSpanWavesPerSimd) void span_kernel(con
         const v4u v = *reinterpret_cast<const v4u*>(mine + read_offset(lane, k));
         line[4 * k] = v.x; line[4 * k + 1] = v.y; line[4 * k + 2] = v.z; line[4 * k + 3] = v.w;
       }
-      if (g + 1 < rows) fetch_row(src + (g + 1) * kRow, slot);
+      if (g + 1 < rows) fetch_row(src + (g + 1) * kStride, slot);
       acc = row_advance(L.row_shift, acc, line_raw(L, lb, sel, line));
     }
   }
-  if (j < extra) {  // the partial last row
+  uint32_t c = 0;
+  if (partial) {  // the partial last row (row rtot = w + rows * G): followed by extra - 1 - j lines and rest
     uint32_t E[kLineWords];
-    load_line(p + rows * kRow, E);
+    load_line(a.bulk + (rtot * kSpanLanes + j) * kSpanLine, E);
     acc = row_advance(L.row_shift, acc, line_raw(L, lb, sel, E));
+    c = gf2_mulmod(a.rest_op, gf2_mulmod(a.span->lane_op[extra - 1 - j], acc));
+  } else if (rows) {  // last line: row w + (rows-1) G, followed by L-1-j lines, then op[w]
+    c = gf2_mulmod(a.op[w], gf2_mulmod(a.span->lane_op[kSpanLanes - 1 - j], acc));
   }
-  // Lane j's last line is followed, within the range, by (extra - 1 - j) mod L lines.
-  const uint32_t after = (extra + kSpanLanes - 1 - j) % kSpanLanes;
-  uint32_t c = (rows || j < extra) ? gf2_mulmod(a.span->lane_op[after], acc) : 0u;
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) c ^= __shfl_xor(c, off, 64);
   if ((j & 63) == 0) L.wave_sum[j / 64] = c;
@@ -250,7 +256,7 @@ __global__ __launch_bounds__(kSpanLanes, kSpanWavesPerSimd) void span_kernel(con
     uint32_t t = 0;
 #pragma unroll
     for (int v = 0; v < kSpanLanes / 64; ++v) t ^= L.wave_sum[v];
-    atomicXor(a.crc, gf2_mulmod(a.op[w], t));
+    atomicXor(a.crc, t);
   }
 }
 
@@ -281,14 +287,17 @@ hipError_t launch_crc_span(const void* data, uint64_t length, uint32_t* crc, con
   a.span = span;
   a.nline = nline;
   a.groups = (uint32_t)groups;
-  // op[w] = x^(8 * (bytes of the ranges after w + rest)); ranges hold q+1 lines (w < r) or q.
-  const uint64_t q = nline / groups, r = nline % groups;
-  const uint32_t step_q = xpow8n(kSpanLine * q), step_q1 = xpow8n(kSpanLine * (q + 1));
-  uint32_t op = xpow8n(rest);
-  for (uint64_t w = groups; w-- > 0;) {
-    a.op[w] = op;
-    op = gf2_mulmod(w < r ? step_q1 : step_q, op);  // w - 1 is followed by w's range as well
-  }
+  a.stride_op = xpow8n((uint64_t)kSpanLine * kSpanLanes * groups);
+  a.rest_op = xpow8n(rest);
+  // op[w]: after workgroup w's last full row r_last come (rtot - 1 - r_last) = (rtot - 1 - w) mod G
+  // full rows, the extra lines and the rest bytes.
+  const uint64_t rtot = nline / kSpanLanes, extra = nline % kSpanLanes;
+  const uint32_t base = xpow8n((uint64_t)kSpanLine * extra + rest), zrow = xpow8n((uint64_t)kSpanLine * kSpanLanes);
+  uint32_t pw[kSpanMaxGroups];  // zrow^d
+  pw[0] = 1u << 31;
+  for (uint64_t d = 1; d < groups; ++d) pw[d] = gf2_mulmod(zrow, pw[d - 1]);
+  for (uint64_t w = 0; w < groups; ++w)
+    a.op[w] = w < rtot ? gf2_mulmod(base, pw[(rtot - 1 - w) % groups]) : 0u;
   hipLaunchKernelGGL(span_kernel, dim3((uint32_t)groups), dim3(kSpanLanes), 0, s, a);
   return hipGetLastError();
 }

@@ -118,14 +118,13 @@ hipError_t launch_fill(void* dst, size_t bytes, uint64_t seed, hipStream_t s);
 
 // Span CRC (efes_crc_span.hip): CRC-32 of one long buffer on the whole GPU.  Bytes per lane per
 // row (64: half a 128-B cache line, measured fastest), lanes per workgroup, the workgroup cap (the host passes each
-// workgroup's combine operator as a kernel argument), and the per-context operator tables:
-// row_shift advances a raw register over one workgroup row (kSpanLanes lines), byte-sliced;
-// lane_op[k] = x^(8*kSpanLine*k) mod P.
+// workgroup's combine operator as a kernel argument), and the per-context operator table
+// lane_op[k] = x^(8*kSpanLine*k) mod P (the row shift depends on the launch's workgroup count and is
+// built by each workgroup from its operator).
 constexpr int kSpanLine = 64;  // bytes per lane per row (round 2 A/B of 16, 32, 48, 64, 128: profiles/r02_span/)
 constexpr int kSpanLanes = 1024;
 constexpr int kSpanMaxGroups = 512;
 struct SpanTables {
-  uint32_t row_shift[4][256];
   uint32_t lane_op[kSpanLanes];
 };
 void build_span_tables(SpanTables* t);  // host

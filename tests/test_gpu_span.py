@@ -155,3 +155,17 @@ def test_span_pieces_on_two_contexts_combine(env):
         assert combine_piece_crcs(pieces) == whole == zlib.crc32(buf.cpu().numpy())
     finally:
         ctxs[1].close()
+
+
+def test_span_random_lengths_against_zlib(env):
+    """Seeded random lengths from 1 byte to 320 MiB (every workgroup count from 1 to the CU count,
+    partial last rows owned by any workgroup of the round-robin), random starts and states."""
+    n_max = 320 << 20
+    buf = _device_bytes(env, n_max + 64, 0x5EED)
+    host = buf.cpu().numpy()
+    rng = random.Random(2026)
+    for _ in range(48):
+        n = int(rng.choice([rng.randrange(1, 1 << 20), rng.randrange(1 << 20, 64 << 20), rng.randrange(64 << 20, n_max)]))
+        off = rng.randrange(0, 16)
+        crc_in = rng.getrandbits(32)
+        assert _span(env, buf, off, n, crc_in) == zlib.crc32(host[off:off + n], crc_in), (n, off, hex(crc_in))

@@ -896,6 +896,37 @@ def mixed_leg(args, rank: int, world: int, ctx, device: str, stream):
             "clock": clock, "note": "makespan set by the 64 MiB chunks' SHA-1 chains (DESIGN_NOTES.md §4 batch planner); not `value`"}
 
 
+def read_ceiling(data, n: int, device: str, stream, reps: int = 3):
+    """The read ceiling of the span leg's own buffer: a pure LDS-DMA nontemporal read of it in the
+    span kernel's shape (tools/readprobe.hip), timed with HIP events on the leg's stream.  The span
+    CRC's rate follows the buffer's allocation, so its fraction is also reported
+    against this."""
+    import ctypes
+
+    import torch
+
+    path = os.path.join(ROOT, "tools", "libreadprobe.so")
+    if not os.path.exists(path):
+        return None
+    lib = ctypes.CDLL(path)
+    lib.readprobe_launch.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p]
+    dev = torch.device(device).index or 0
+    groups = torch.cuda.get_device_properties(dev).multi_processor_count
+    usable = n - n % (64 << 10)
+    if lib.readprobe_launch(dev, data.data_ptr(), usable, groups, stream.cuda_stream) != 0:  # warm-up
+        return None
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        lib.readprobe_launch(dev, data.data_ptr(), usable, groups, stream.cuda_stream)
+    e1.record(stream)
+    stream.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    return {"value": round(usable / (ms * 1e-3) / 1e9, 1), "unit": "GB/s",
+            "kind": "LDS-DMA nontemporal read of the same buffer, the span kernel's shape (tools/readprobe.hip)",
+            "microbenchmark": "7.0-7.2 TB/s on a fresh buffer (tools/microbench/mb_glds, profiles/r05_span_nt/)"}
+
+
 def span_crc_leg(args, ctx, device: str, stream, gib: int = 16, reps: int = 5):
     """CRC-32 alone of ONE object resident in HBM (efes_crc32_span, segment-
     parallel over all CUs), against the HBM roofline; the first GiB is checked against zlib, and the
@@ -925,6 +956,7 @@ def span_crc_leg(args, ctx, device: str, stream, gib: int = 16, reps: int = 5):
         stream.synchronize()
         clock = clk.stop()
         ms = e0.elapsed_time(e1) / reps
+        ceiling = read_ceiling(data, n, device, stream)
         st.zero_()
         ctx.crc32_span(data.data_ptr(), 1 << 30, st.data_ptr(), stream.cuda_stream)
         stream.synchronize()
@@ -943,9 +975,8 @@ def span_crc_leg(args, ctx, device: str, stream, gib: int = 16, reps: int = 5):
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 4), "ms_per_call": round(ms, 3),
                          "traffic": load_traffic("span_kernel", f"{gib}GiB:span"),
-                         "read_ceiling": {"value": 7100.0, "unit": "GB/s",
-                                          "source": "LDS-DMA nontemporal reads alone, 7.0-7.2 TB/s "
-                                                    "(tools/microbench/mb_glds, profiles/r05_span_nt/)"}},
+                         "read_ceiling": ceiling,
+                         "frac_of_read_ceiling": None if not ceiling else round(achieved / ceiling["value"], 4)},
             "cpu_port_1core": {"value": round((1 << 30) / cpu_s / GiB, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
                                "sample": "oracle crc32digest.Write (slicing-by-8, crc32.go:153-169) over the first GiB"},
             "crc_matches_zlib": ok, "clock": clock, "note": "HIP events on the launch stream; not `value`"}

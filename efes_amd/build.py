@@ -86,6 +86,14 @@ def build_tools() -> list[str]:
         os.replace(so + ".tmp", so)
     if os.path.exists(so):
         out.append(so)
+    src = os.path.join(ROOT, "tools", "readprobe.hip")  # bench.py's read ceiling of the span leg's buffer
+    so = os.path.join(ROOT, "tools", "libreadprobe.so")
+    if os.path.exists(src) and _stale(so, [src]):
+        subprocess.run([hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", src, "-o", so + ".tmp"],
+                       check=True)
+        os.replace(so + ".tmp", so)
+    if os.path.exists(so):
+        out.append(so)
     src = os.path.join(ROOT, "tools", "bench_receiver.cpp")
     exe = os.path.join(ROOT, "tools", "bench_receiver")
     if os.path.exists(src) and _stale(exe, [src, RECEIVER_LIB, RECEIVER_HDR, LIB]):

@@ -650,6 +650,9 @@ class ClockMeter:
                 s = sorted(self._samples)
                 out.update({"smi_mhz_mean": round(sum(s) / len(s), 1), "smi_mhz_min": round(s[0], 1),
                             "smi_mhz_max": round(s[-1], 1), "smi_samples": len(s)})
+                if len(s) < 25:  # amdsmi's clock lags its window: a region of a few ms reads the clock before it
+                    out["smi_note"] = ("fewer than 25 samples over the region: amdsmi's reading lags and is not "
+                                       "this region's clock (span leg: profiles/r05_span_clock/summary.txt)")
         # the probe: within 0.1-1 % of GRBM_GUI_ACTIVE in the same run; the amdsmi mean strays by up to
         # 6 % (it samples clock transients between launches; profiles/r05_clock/calibration.txt)
         out["mhz"] = out.get("probe_mhz", out.get("smi_mhz_mean"))

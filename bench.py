@@ -116,7 +116,34 @@ def parse_args(argv=None):
     p.add_argument("--all-ranks-on-device0", action="store_true",
                    help="rehearse the N>1 path on a 1-GPU box (use with --dist-backend gloo)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="minimum CPU work in the cpu_baseline sample")
+    p.add_argument("--latency-uploads", default="1,16,64,128,192,256",
+                   help="patch_latency leg: uploads in flight of each point")
+    p.add_argument("--drain-workers", default="1,16,64,128,192,256,512", help="drain_path leg: workers of each point")
+    p.add_argument("--watchdog", type=float, default=0.0,
+                   help="dump every thread's Python stack to stderr after this many seconds (faulthandler; "
+                        "0 = off; the GPU test of this file arms it)")
     return p.parse_args(argv)
+
+
+class Legs:
+    """Runs the side legs one after the other, logging each start and end to stderr (so a stalled
+    run names its leg) and keeping their wall seconds for the output line (`leg_seconds`)."""
+
+    def __init__(self):
+        self.seconds = {}
+        self.t0 = time.perf_counter()
+
+    def run(self, name: str, fn, *a, **kw):
+        t = time.perf_counter()
+        print(f"[bench] {name}: start at {t - self.t0:.1f} s", file=sys.stderr, flush=True)
+        r = fn(*a, **kw)
+        self.seconds[name] = round(time.perf_counter() - t, 2)
+        print(f"[bench] {name}: done in {self.seconds[name]} s", file=sys.stderr, flush=True)
+        return r
+
+
+def _ints(csv: str) -> tuple:
+    return tuple(int(x) for x in csv.split(",") if x.strip())
 
 
 def host_threads() -> int:
@@ -293,7 +320,7 @@ def go_surface_leg(uploads=None):
     return res
 
 
-def patch_latency_leg():
+def patch_latency_leg(uploads=(1, 16, 64, 128, 192, 256)):
     """Per-PATCH latency of one 4 MiB PATCH (saveFile's hashing: MultiWriter CRC-then-SHA-1 Writes in
     32 KiB buffers, then both Sums) with 1, 16 and 256 uploads in flight: the unchanged Go surface on
     the GPU (tools/bench_go_surface, one PATCH per request thread, fused pairs) against the CPU port
@@ -311,7 +338,8 @@ def patch_latency_leg():
         return json.loads(r.stdout.strip().splitlines()[-1])
 
     points = []
-    for k, rounds in ((1, 20), (16, 8), (64, 6), (128, 4), (192, 4), (256, 4)):
+    for k in uploads:
+        rounds = 20 if k == 1 else 8 if k <= 16 else 6 if k <= 64 else 4
         g = run([os.path.join(ROOT, "tools", "bench_go_surface"), str(k), str(k * rounds), str(4 << 20), str(32 << 10),
                  "1", "1", "256", "1024"])
         c = run([os.path.join(ROOT, "oracle", "patch_cpu"), str(k), str(4 << 20), "3"])
@@ -557,6 +585,36 @@ N_SIMD = 1024
 VALU_CYC = 4
 
 
+SMI_JOIN_S = 2.0  # bound on waiting for the amdsmi poll thread (it polls every 2 ms)
+_SMI_STATE = {"module": None, "tried": False, "stuck": False}
+
+
+def _smi_module():
+    """amdsmi, initialised ONCE per process (amdsmi_shut_down registered at exit), or None when it
+    is absent or refuses.  Every ClockMeter shares it."""
+    import atexit
+
+    if not _SMI_STATE["tried"]:
+        _SMI_STATE["tried"] = True
+        try:
+            import amdsmi
+
+            amdsmi.amdsmi_init()
+        except Exception:  # noqa: BLE001 -- amdsmi absent or refused: the probe alone
+            return None
+        _SMI_STATE["module"] = amdsmi
+
+        def _shut_down():
+            if not _SMI_STATE["stuck"]:  # a poll thread still inside amdsmi: leave the library alone
+                try:
+                    amdsmi.amdsmi_shut_down()
+                except Exception:  # noqa: BLE001
+                    pass
+
+        atexit.register(_shut_down)
+    return _SMI_STATE["module"]
+
+
 class ClockMeter:
     """The effective engine clock over a timed region (the VALU-issue ceilings scale with it), read two
     ways at once:
@@ -565,7 +623,9 @@ class ClockMeter:
                CU (memtime counters of different units have different offsets), median over CUs;
       smi   -- amdsmi's per-XCD current_gfxclk, polled every 2 ms by a host thread, averaged.
     Calibrated against GRBM_GUI_ACTIVE / 8 / ns of the same kernels (profiles/r05_clock/): `mhz` is
-    the probe's (within 1 %), the amdsmi mean only when the probe library is missing."""
+    the probe's (within 1 %), the amdsmi mean only when the probe library is missing.  amdsmi is
+    initialised once per process (_smi_module) and the poll thread's join is bounded (SMI_JOIN_S):
+    neither half can hold the bench (DESIGN_NOTES.md "The r05_check hang")."""
 
     def __init__(self, dev_index: int):
         import ctypes
@@ -586,45 +646,47 @@ class ClockMeter:
                     bdf = buf.value.decode().lower()
             except (OSError, AttributeError):
                 self.probe = None
+        self.bdf = bdf
+        amdsmi = _smi_module()
         try:
-            import amdsmi
-
-            amdsmi.amdsmi_init()
-            handles = amdsmi.amdsmi_get_processor_handles()
-            pick = handles[dev_index] if dev_index < len(handles) else None
-            for h in handles:
-                if bdf and str(amdsmi.amdsmi_get_gpu_device_bdf(h)).lower() == bdf:
-                    pick = h
-            if pick is not None:
-                amdsmi.amdsmi_get_gpu_metrics_info(pick)
-                self.smi = (amdsmi, pick)
-        except Exception:  # noqa: BLE001 -- amdsmi absent or refused: the probe alone
+            if amdsmi is not None:
+                handles = amdsmi.amdsmi_get_processor_handles()
+                pick = handles[dev_index] if dev_index < len(handles) else None
+                for h in handles:
+                    if bdf and str(amdsmi.amdsmi_get_gpu_device_bdf(h)).lower() == bdf:
+                        pick = h
+                if pick is not None:
+                    amdsmi.amdsmi_get_gpu_metrics_info(pick)
+                    self.smi = (amdsmi, pick)
+        except Exception:  # noqa: BLE001 -- amdsmi refused: the probe alone
             self.smi = None
         self._thread = None
         self._samples = []
-        self._stop = False
+        self._stop = None
         self._marked = False
+        self.smi_dropped = None
 
-    def _poll(self):
+    def _poll(self, stop, samples):
         amdsmi, h = self.smi
-        while not self._stop:
+        while not stop.is_set():
             try:
                 m = amdsmi.amdsmi_get_gpu_metrics_info(h)
                 v = [float(x) for x in m.get("current_gfxclks", []) if isinstance(x, (int, float)) and 0 < x < 65535]
                 if v:
-                    self._samples.append(sum(v) / len(v))
+                    samples.append(sum(v) / len(v))
             except Exception:  # noqa: BLE001
                 return
-            time.sleep(0.002)
+            stop.wait(0.002)
 
     def start(self, stream: int):
         """Before the region's first launch on `stream` (a hipStream_t handle)."""
         import threading
 
-        self._samples, self._stop = [], False
+        self._samples, self._stop = [], threading.Event()
         self._marked = self.probe is not None and self.probe.clockprobe_mark(self.dev, stream, 0) == 0
         if self.smi:
-            self._thread = threading.Thread(target=self._poll, daemon=True)
+            self._thread = threading.Thread(target=self._poll, args=(self._stop, self._samples), daemon=True,
+                                            name="clock-smi-poll")
             self._thread.start()
 
     def end(self, stream: int):
@@ -643,10 +705,19 @@ class ClockMeter:
                 out.update({"probe_mhz": round(mhz.value, 1), "probe_seconds": round(sec.value, 4),
                             "probe_cus": n.value})
         if self._thread:
-            self._stop = True
-            self._thread.join()
+            self._stop.set()
+            self._thread.join(SMI_JOIN_S)
+            if self._thread.is_alive():
+                # an amdsmi call that does not return must not hold the bench: the thread is a
+                # daemon, this meter stops using amdsmi for the rest of the process, and the
+                # process-wide amdsmi_shut_down at exit is skipped (DESIGN_NOTES.md "r05_check hang")
+                _SMI_STATE["stuck"] = True
+                self.smi, self.smi_dropped = None, f"amdsmi poll did not return within {SMI_JOIN_S} s; dropped"
+                self._samples = []
             self._thread = None
-            if self._samples:
+            if self.smi_dropped:
+                out["smi_note"] = self.smi_dropped
+            elif self._samples:
                 s = sorted(self._samples)
                 out.update({"smi_mhz_mean": round(sum(s) / len(s), 1), "smi_mhz_min": round(s[0], 1),
                             "smi_mhz_max": round(s[-1], 1), "smi_samples": len(s)})
@@ -987,6 +1058,11 @@ def span_crc_leg(args, ctx, device: str, stream, gib: int = 16, reps: int = 5):
 
 def main(argv=None):
     args = parse_args(argv)
+    if args.watchdog > 0:
+        import faulthandler
+
+        faulthandler.dump_traceback_later(args.watchdog, exit=False)  # all threads' stacks to stderr
+    legs = Legs()
     import torch
 
     from efes_amd import MODE_AUTO, MODE_DEEP, MODE_WIDE
@@ -1025,6 +1101,7 @@ def main(argv=None):
         if dist:
             dist.destroy_process_group()
         return
+    print(f"[bench] headline ({args.workload}): start", file=sys.stderr, flush=True)
     with torch.cuda.stream(stream):
         data, batches, step_bytes, config = make_workload(args, rank, world, ctx, device, stream)
         if mode == MODE_PLAN:
@@ -1032,6 +1109,7 @@ def main(argv=None):
                 b.make_plan()  # host-side planning stays outside the timed region
         steps = args.steps if len(batches) == 1 else len(batches)
         wall, kernel_ms, clock = run_timed(batches, steps, args.warmup, mode, device, stream, dist, args.progress)
+    print(f"[bench] headline: {steps} steps in {wall:.3f} s on this rank", file=sys.stderr, flush=True)
     wall = max_over_ranks(wall, device if args.dist_backend == "nccl" else None)  # slowest rank
 
     bytes_timed = sum(step_bytes[k % len(step_bytes)] for k in range(steps))
@@ -1086,35 +1164,37 @@ def main(argv=None):
     if args.workload == "chunks4m":
         n, chunk = args.chunks, args.chunk_bytes
         if args.host_inclusive == "on" or (args.host_inclusive == "auto" and world == 1):
-            out["host_inclusive"] = host_inclusive(ctx, data, n, chunk, not args.sha1_only, args.segment_bytes,
-                                                   batches[0])
+            out["host_inclusive"] = legs.run("host_inclusive", host_inclusive, ctx, data, n, chunk, not args.sha1_only,
+                                                   args.segment_bytes, batches[0])
         if not args.sha1_only and (args.sha1_leg == "on" or (args.sha1_leg == "auto" and world == 1)):
-            out["sha1_only_config"] = sha1_only_leg(args, ctx, data, batches[0], device, stream)
+            out["sha1_only_config"] = legs.run("sha1_only_config", sha1_only_leg, args, ctx, data, batches[0], device, stream)
         if args.ingest_leg in ("on", "auto"):
-            out["ingest_config"] = ingest_leg(args, rank, world, ctx, device, stream, MODE_AUTO, dist)
+            out["ingest_config"] = legs.run("ingest_config", ingest_leg, args, rank, world, ctx, device, stream, MODE_AUTO,
+                                            dist)
         if args.uploads_leg == "on" or (args.uploads_leg == "auto" and world == 1):
             a = argparse.Namespace(**vars(args))
             a.upload_threads, a.uploads, a.open_per_thread, a.upload_bytes = 32, 8192, 256, 4 << 20
-            out["uploads_path"] = uploads_workload(a, ctx)
+            out["uploads_path"] = legs.run("uploads_path", uploads_workload, a, ctx)
         if args.go_surface_leg == "on" or (args.go_surface_leg == "auto" and world == 1):
-            out["go_surface_path"] = go_surface_leg(out.get("uploads_path"))
+            out["go_surface_path"] = legs.run("go_surface_path", go_surface_leg, out.get("uploads_path"))
         if args.latency_leg == "on" or (args.latency_leg == "auto" and world == 1):
-            out["patch_latency"] = patch_latency_leg()
+            out["patch_latency"] = legs.run("patch_latency", patch_latency_leg, _ints(args.latency_uploads))
         if args.receiver_leg == "on" or (args.receiver_leg == "auto" and world == 1):
-            out["receiver_path"] = receiver_leg()
+            out["receiver_path"] = legs.run("receiver_path", receiver_leg)
         if args.drain_leg == "on" or (args.drain_leg == "auto" and world == 1):
-            out["drain_path"] = drain_leg()
+            out["drain_path"] = legs.run("drain_path", drain_leg, _ints(args.drain_workers))
         if args.concurrency_leg == "on" or (args.concurrency_leg == "auto" and world == 1):
-            out["concurrency"] = concurrency_leg(args, ctx, device, stream)
+            out["concurrency"] = legs.run("concurrency", concurrency_leg, args, ctx, device, stream)
         if args.mixed_leg == "on" or (args.mixed_leg == "auto" and world == 1):
-            out["mixed_config"] = mixed_leg(args, rank, world, ctx, device, stream)
+            out["mixed_config"] = legs.run("mixed_config", mixed_leg, args, rank, world, ctx, device, stream)
         if args.span_leg == "on" or (args.span_leg == "auto" and world == 1):
-            out["span_crc"] = span_crc_leg(args, ctx, device, stream)
+            out["span_crc"] = legs.run("span_crc", span_crc_leg, args, ctx, device, stream)
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             threads = args.cpu_threads or host_threads()
-            out["cpu_baseline"] = cpu_baseline(batches[0], data, min(n, args.cpu_max_chunks), chunk, threads,
-                                               not args.sha1_only, args.cpu_seconds)
-            out["config0_cpu"] = config0_cpu(data, chunk)
+            out["cpu_baseline"] = legs.run("cpu_baseline", cpu_baseline, batches[0], data, min(n, args.cpu_max_chunks), chunk,
+                                           threads, not args.sha1_only, args.cpu_seconds)
+            out["config0_cpu"] = legs.run("config0_cpu", config0_cpu, data, chunk)
+    out["leg_seconds"] = legs.seconds
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:

@@ -794,17 +794,38 @@ def test_upload_queue_limits(env):
 
 
 def test_bench_emits_driver_json(env):
-    """bench.py's contract keys on a tiny configuration (the driver parses this line)."""
+    """bench.py's contract keys on a tiny configuration (the driver parses this line).
+
+    The child diagnoses its own stall (round 5's r05_check hang lost the child's stack): it runs
+    with faulthandler armed (`--watchdog`: every thread's stack to stderr before this test gives
+    up), logs each leg's start and end to stderr, and is killed with its whole process group at
+    CHILD_S -- before pytest's own 120-s limit -- so the assertion message carries its stderr and
+    says whether the JSON line was printed (a stall after it is the process's exit, not a leg)."""
     import json
     import os
+    import signal
     import subprocess
     import sys
+    # budget: 70.7 s with every leg at its default points on the r06_check box (patch_latency 25.5 s and
+    # drain_path 15.6 s of it, CPU-bound harnesses); their shortest points keep each leg exercised
+    CHILD_S, WATCHDOG_S = 108, 95
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--chunks", "16", "--chunk-bytes", "65536",
-                          "--steps", "2", "--warmup", "1", "--cpu-seconds", "0.1", "--segment-bytes", "16384",
-                          "--mixed-leg", "off", "--uploads-leg", "off"],
-                         capture_output=True, text=True, timeout=600, check=True).stdout
+    cmd = [sys.executable, "-X", "faulthandler", os.path.join(root, "bench.py"), "--chunks", "16",
+           "--chunk-bytes", "65536", "--steps", "2", "--warmup", "1", "--cpu-seconds", "0.1", "--segment-bytes", "16384",
+           "--mixed-leg", "off", "--uploads-leg", "off", "--latency-uploads", "1,16", "--drain-workers", "1,64",
+           "--watchdog", str(WATCHDOG_S)]
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, start_new_session=True)
+    try:
+        out, err = p.communicate(timeout=CHILD_S)
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, signal.SIGKILL)  # bench.py and the harness binaries it started
+        out, err = p.communicate()
+        printed = any(line.startswith("{") for line in out.splitlines())
+        pytest.fail(f"bench.py did not exit within {CHILD_S} s (JSON line printed: {printed}); its stderr:\n"
+                    f"{err[-12000:]}")
+    assert p.returncode == 0, f"bench.py exited {p.returncode}; its stderr:\n{err[-12000:]}"
     d = json.loads(out.strip().splitlines()[-1])
+    print("leg seconds:", d.get("leg_seconds"))  # the test's time budget, per leg (-s / the log shows it)
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
               "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
         assert k in d, k

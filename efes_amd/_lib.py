@@ -104,6 +104,7 @@ SIGNATURES = {
     "efes_strerror": (ctypes.c_char_p, [_I]),
     "efes_abi_version": (_I, []),
     "efes_sha1_state_init": (None, [_P(Sha1State)]),
+    "efes_device_count": (_I, []),
     "efes_ctx_create": (_I, [_I, _P(_VP)]),
     "efes_ctx_destroy": (None, [_VP]),
     "efes_ctx_device": (_I, [_VP]),

@@ -172,6 +172,15 @@ void efes_sha1_state_init(efes_sha1_state* s) {  // sha1.go:36-44 (x untouched, 
   s->len = 0;
 }
 
+int efes_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) {
+    efes::clear_last_error();  // no runtime / no devices: a count of 0, not a later launch's error
+    return 0;
+  }
+  return n > 0 ? n : 0;
+}
+
 int efes_ctx_create(int device, efes_ctx** out) {
   if (!out) return EFES_ERR_ARG;
   *out = nullptr;

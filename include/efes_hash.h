@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define EFES_ABI_VERSION 6
+#define EFES_ABI_VERSION 7
 
 /* ---- error codes ---------------------------------------------------------------- */
 #define EFES_OK 0
@@ -70,7 +70,13 @@ void efes_sha1_state_init(efes_sha1_state* s);
 /* ---- context ----------------------------------------------------------------------- */
 typedef struct efes_ctx efes_ctx;
 
-/* Binds one GPU (HIP device ordinal), uploads the CRC tables, creates a stream. */
+/* HIP devices visible to the process, of any architecture (ABI 7): 0 when there are none or the
+ * runtime fails.  A binding opens every ordinal below it and SKIPS the ones efes_ctx_create refuses
+ * (EFES_ERR_NO_DEVICE for a non-gfx950 card, EFES_ERR_HIP / EFES_ERR_NOMEM for one that fails to
+ * initialise), so one bad GPU does not hide the GPUs after it (go/hash_gpu.go pool()). */
+int efes_device_count(void);
+/* Binds one GPU (HIP device ordinal), uploads the CRC tables, creates a stream.  EFES_ERR_ARG for an
+ * ordinal outside [0, efes_device_count()), EFES_ERR_NO_DEVICE for a device that is not gfx950. */
 int efes_ctx_create(int device, efes_ctx** out);
 void efes_ctx_destroy(efes_ctx* ctx);
 int efes_ctx_device(const efes_ctx* ctx);

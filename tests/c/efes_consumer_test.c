@@ -18,6 +18,11 @@
  *   pairs   -- fused MultiWriter digest pairs (ABI 6) driven through every call pattern that splits
  *              them, from T threads, each sync point against the oracle.
  *   errors  -- errInvalidDigest and the Go panic states surface as error codes.
+ *   enumerate <ordinals> -- go/hash_gpu.go pool()'s device loop over a given ordinal list (a failing
+ *              ordinal in the middle stands in for a GPU whose context does not open): failures are
+ *              reported and skipped, never the end of the loop; the contexts that opened form one
+ *              efes_pool and the patch uploads run on pooled digests (efes_*_new_pool); every context
+ *              of the pool, the one after the failure included, must hash.
  * Prints one line "efes_consumer_test ok ..." and exits 0, or names the first mismatch.
  */
 #include <pthread.h>
@@ -30,6 +35,7 @@
 #include "../../oracle/efes_oracle.h"
 
 static efes_ctx* g_ctx;
+static efes_pool* g_pool; /* enumerate: pooled digests (hash_gpu.go) instead of g_ctx's */
 static int g_fail;
 static pthread_mutex_t g_mu = PTHREAD_MUTEX_INITIALIZER;
 
@@ -75,7 +81,9 @@ static void* patch_worker(void* p) {
       const int last = off + n == len;
       efes_sha1* sha = NULL;
       efes_crc32* crc = NULL;
-      if (efes_sha1_new(g_ctx, &sha) || efes_crc32_new(g_ctx, &crc)) { FAIL("new"); break; }
+      const int rn = g_pool ? efes_sha1_new_pool(g_pool, &sha) || efes_crc32_new_pool(g_pool, &crc)
+                            : efes_sha1_new(g_ctx, &sha) || efes_crc32_new(g_ctx, &crc);
+      if (rn) { FAIL("new"); break; }
       if (off > 0) {  /* ReadFileInfo (filereceiver.go:182) */
         if (efes_sha1_unmarshal_text(sha, sha_text, 200) || efes_crc32_unmarshal_text(crc, crc_text, 8)) {
           FAIL("unmarshal upload %d.%d", a->id, u);
@@ -382,7 +390,59 @@ static int test_errors(void) {
   return !g_fail;
 }
 
+/* ---- enumerate: go/hash_gpu.go pool() -------------------------------------------------------- */
+static int test_enumerate(const char* list, int threads, int uploads) {
+  enum { MAXC = 16 };
+  efes_ctx* ctxs[MAXC];
+  int devs[MAXC], opened = 0, listed = 0, skipped = 0;
+  const int visible = efes_device_count();
+  for (const char* p = list; *p && opened < MAXC;) {
+    char* end;
+    const int dev = (int)strtol(p, &end, 10);
+    if (end == p) break;
+    p = *end == ',' ? end + 1 : end;
+    ++listed;
+    efes_ctx* c = NULL;
+    const int rc = efes_ctx_create(dev, &c);
+    if (rc != EFES_OK) { /* hash_gpu.go: log, count, and go on with the next GPU */
+      printf("enumerate: device %d skipped: %s\n", dev, efes_strerror(rc));
+      if (c) FAIL("efes_ctx_create failed but returned a context");
+      ++skipped;
+      continue;
+    }
+    ctxs[opened] = c;
+    devs[opened++] = dev;
+  }
+  if (!opened || !skipped) {
+    FAIL("enumerate: %d opened, %d skipped of %d listed (want both)", opened, skipped, listed);
+    return 0;
+  }
+  int rc = efes_pool_create(ctxs, (uint32_t)opened, &g_pool);
+  if (rc) { FAIL("efes_pool_create: %s", efes_strerror(rc)); return 0; }
+  const int ok = test_patch(threads, uploads);
+  printf("enumerate: visible %d, listed %d, opened %d, skipped %d; jobs per context:", visible, listed, opened,
+         skipped);
+  for (int i = 0; i < opened; ++i) {
+    efes_queue_stats st;
+    if (efes_pool_stats(g_pool, (uint32_t)i, &st)) FAIL("efes_pool_stats %d", i);
+    printf(" %d:%llu", devs[i], (unsigned long long)st.jobs);
+    if (ok && st.jobs == 0) FAIL("context %d (device %d) of the pool hashed nothing", i, devs[i]);
+  }
+  printf("\n");
+  efes_pool_destroy(g_pool);
+  g_pool = NULL;
+  for (int i = 0; i < opened; ++i) efes_ctx_destroy(ctxs[i]);
+  return !g_fail;
+}
+
 int main(int argc, char** argv) {
+  if (argc > 2 && !strcmp(argv[1], "enumerate")) {
+    oracle_crc32_init_tables();
+    const int ok = test_enumerate(argv[2], argc > 3 ? atoi(argv[3]) : 16, argc > 4 ? atoi(argv[4]) : 4);
+    if (!ok) return 1;
+    printf("efes_consumer_test ok (enumerate)\n");
+    return 0;
+  }
   const int threads = argc > 1 ? atoi(argv[1]) : 16;
   const int uploads = argc > 2 ? atoi(argv[2]) : 6;
   if (threads < 1 || threads > 64) return 2;

@@ -178,14 +178,14 @@ def test_crc32_combine_matches_concatenation(efes_lib):
 
 
 def test_integration_doc_binds_only_declared_symbols():
-    """The cgo binding in INTEGRATION.md only calls entry points include/efes_hash.h declares."""
-    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
-    used = set(re.findall(r"\bC\.(efes_\w+)\s*\(", doc))
-    assert len(used) >= 15
-    missing = sorted(used - set(declared_functions()))
-    assert not missing, missing
-    for const in set(re.findall(r"\bC\.(EFES_\w+)", doc)):
-        assert re.search(r"#define\s+%s\b" % const, open(HEADER).read()), const
+    """The cgo binding (go/*.go) and INTEGRATION.md only call entry points include/efes_hash.h declares."""
+    for text in [open(os.path.join(ROOT, "INTEGRATION.md")).read(), "\n".join(_go_sources().values())]:
+        used = set(re.findall(r"\bC\.(efes_\w+)\s*\(", text))
+        missing = sorted(used - set(declared_functions()))
+        assert not missing, missing
+        for const in set(re.findall(r"\bC\.(EFES_\w+)", text)):
+            assert re.search(r"#define\s+%s\b" % const, open(HEADER).read()), const
+    assert len(set(re.findall(r"\bC\.(efes_\w+)\s*\(", "\n".join(_go_sources().values())))) >= 30
 
 
 def test_plan_struct_layout_matches_header(tmp_path, efes_lib):
@@ -220,8 +220,9 @@ def test_auto_mode_by_job_count(efes_lib):
 
 
 def test_integration_doc_covers_every_declared_symbol():
-    """Every entry point of include/efes_hash.h appears in INTEGRATION.md (cgo binding or table)."""
-    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    """Every entry point of include/efes_hash.h appears in INTEGRATION.md's tables or the cgo binding
+    it ships (go/*.go)."""
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read() + "\n".join(_go_sources().values())
     missing = [n for n in declared_functions() if not re.search(r"\b%s\b" % n, doc)]
     assert not missing, missing
 
@@ -290,14 +291,25 @@ def test_integration_doc_two_build_targets():
         assert "CGO_ENABLED=0" in open(os.path.join(ref, ".goreleaser.yml")).read().split("\n")[8]
 
 
-# ---- the Go binding of INTEGRATION.md (no Go toolchain here: its ownership rules, checked as text) --
+# ---- the Go binding, go/*.go (no Go toolchain here: its ownership rules, checked as text) -----------
 REF = "/root/reference"
 DIGEST_FILES = ("sha1.go", "sha1_efes.go", "crc32.go", "crc32_efes.go")  # replaced under -tags efesgpu
+GO_DIR = os.path.join(ROOT, "go")
+
+
+def _go_sources() -> dict:
+    """{file name: source} of the binding files a maintainer drops into the reference (go/*.go)."""
+    return {f: open(os.path.join(GO_DIR, f)).read() for f in sorted(os.listdir(GO_DIR)) if f.endswith(".go")}
+
+
+def _binding() -> str:
+    return _go_sources()["hash_gpu.go"]
 
 
 def _go_blocks():
+    """Every piece of Go the integration ships: the go/*.go files and any Go left in INTEGRATION.md."""
     doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
-    return re.findall(r"```go\n(.*?)```", doc, flags=re.S)
+    return list(_go_sources().values()) + re.findall(r"```go\n(.*?)```", doc, flags=re.S)
 
 
 def _go_funcs(src: str):
@@ -369,7 +381,7 @@ def test_go_binding_replaces_the_digest_files_whole():
         assert f"`{f}`" in doc[doc.index("## 1. Build"):doc.index("## 3.")], f
     if not os.path.isdir(REF):
         pytest.skip("reference not present")
-    binding = next(b for b in _go_blocks() if "//go:build efesgpu" in b)
+    binding = "\n".join(_go_sources().values())
     mine = {(t, n) for r, t, n, _ in _go_funcs(binding) if r}
     mine_top = {n for r, _t, n, _ in _go_funcs(binding) if not r} | set(re.findall(r"^var (\w+)", binding, flags=re.M)) \
         | set(re.findall(r"^type (\w+)", binding, flags=re.M))
@@ -418,10 +430,77 @@ def test_integration_load_rule_and_gauges():
     doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
     rule = doc[doc.index("**Load rule for `efes-server`.**"):doc.index("## 2.")]
     assert "patch_latency" in rule and "8.5 × C uploads are in flight" in rule
-    binding = next(b for b in _go_blocks() if "//go:build efesgpu" in b)
+    binding = _binding()
     registered = set(re.findall(r'prometheus\.NewDesc\("(efes_gpu_\w+)"', binding))
     named = set(re.findall(r"`(efes_gpu_\w+)(?:\{gpu\})?`", rule))
     assert named and named <= registered, (named, registered)
     assert "prometheus.MustRegister(gpuCollector{})" in binding
     collect = next(body for r, t, n, body in _go_funcs(binding) if n == "Collect")
     assert "pool()" not in collect and "gpuReady.Load()" in collect
+
+
+def test_go_files_are_the_tagged_drop_in():
+    """the cgo shim ships as files.  Every go/*.go file is `package main` under the
+    `efesgpu` build constraint (its first line, then a blank line, as `go build` requires), and
+    INTEGRATION.md points at the files instead of embedding the binding."""
+    srcs = _go_sources()
+    assert {"hash_gpu.go", "upload_gpu.go"} <= set(srcs)
+    for name, src in srcs.items():
+        assert src.startswith("//go:build efesgpu\n\n"), name
+        assert re.search(r"^package main$", src, flags=re.M), name
+        assert 'import "C"' in src, name
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    assert "go/hash_gpu.go" in doc and "go/efesgpu_build_tags.patch" in doc and "go/upload_gpu.go" in doc
+    # the code lives in the files, not in the document: no fenced Go in it defines a digest method
+    assert not [b for b in re.findall(r"```go\n(.*?)```", doc, flags=re.S) if re.search(r"^func |^package ", b, flags=re.M)]
+    defined = {n for src in srcs.values() for r, _t, n, _ in _go_funcs(src) if r is None}
+    assert len(defined) == len([n for src in srcs.values() for r, _t, n, _ in _go_funcs(src) if r is None])
+
+
+def test_build_tag_patch_applies_to_the_reference(tmp_path):
+    """go/efesgpu_build_tags.patch puts `//go:build !efesgpu` and a blank line above line 1 of exactly the
+    four digest files (sha1.go:1, sha1_efes.go:1, crc32.go:1, crc32_efes.go:1) and nothing else;
+    `patch --dry-run`, then the real apply, on a copy of the four reference files."""
+    import shutil
+
+    pt = os.path.join(GO_DIR, "efesgpu_build_tags.patch")
+    text = open(pt).read()
+    files = re.findall(r"^\+\+\+ b/(\S+)$", text, flags=re.M)
+    assert sorted(files) == sorted(DIGEST_FILES)
+    added = re.findall(r"^\+(?!\+\+ )(.*)$", text, flags=re.M)
+    assert added == ["//go:build !efesgpu", ""] * 4
+    assert not re.findall(r"^-(?!-- )", text, flags=re.M)  # removes nothing
+    if not shutil.which("patch"):
+        pytest.skip("patch(1) not installed")
+    if not os.path.isdir(REF):
+        pytest.skip("reference not present")
+    for f in DIGEST_FILES:
+        shutil.copy(os.path.join(REF, f), tmp_path / f)
+    r = subprocess.run(["patch", "-p1", "--dry-run", "-i", pt], cwd=tmp_path, capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    r = subprocess.run(["patch", "-p1", "-i", pt], cwd=tmp_path, capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    for f in DIGEST_FILES:
+        got = (tmp_path / f).read_text()
+        assert got == "//go:build !efesgpu\n\n" + open(os.path.join(REF, f)).read(), f
+
+
+def test_go_pool_opens_every_device_and_skips_failures():
+    """pool() loops to efes_device_count(), and a device whose context fails
+    (EFES_ERR_NO_DEVICE / _HIP / _NOMEM on a GPU that exists) is logged, counted and SKIPPED --
+    `continue`, never `break` -- so one bad GPU 3 does not leave GPUs 4-7 unused; the collector
+    publishes efes_gpu_devices_visible / efes_gpu_devices_opened and labels per-GPU series by HIP
+    ordinal.  (The same loop runs on a GPU in tests/c/efes_consumer_test.c `enumerate`.)"""
+    b = _binding()
+    body = next(body for r, t, n, body in _go_funcs(b) if n == "pool")
+    assert "C.efes_device_count()" in body
+    loop = body[body.index("for dev := 0; dev < gpuVisible; dev++"):]
+    fail = loop[loop.index("!= C.EFES_OK {"):]
+    fail = fail[:fail.index("}")]
+    assert "continue" in fail and "break" not in loop.split("gpuCtxs = append")[0]
+    assert "gpuSkipped = append" in fail and "gpuLog.Warningln" in fail
+    assert "gpuDevs = append(gpuDevs, dev)" in loop
+    registered = set(re.findall(r'prometheus\.NewDesc\("(efes_gpu_\w+)"', b))
+    assert {"efes_gpu_devices_visible", "efes_gpu_devices_opened"} <= registered
+    collect = next(body for r, t, n, body in _go_funcs(b) if n == "Collect")
+    assert "len(gpuCtxs)" in collect and "gpuVisible" in collect and "strconv.Itoa(gpuDevs[i])" in collect

@@ -157,7 +157,13 @@ def build_lifecycle_test() -> str:
     deps = srcs + [os.path.join(ROOT, "tests", "c", "efes_lifecycle_test.c"), os.path.join(ROOT, "tools", "asan_build.sh"),
                    os.path.join(ROOT, "oracle", "liboracle.so")] + [os.path.join(ROOT, "include", h) for h in PUBLIC_HEADERS]
     if _stale(exe, deps):
-        subprocess.run(["bash", os.path.join(ROOT, "tools", "asan_build.sh")], check=True)
+        try:
+            subprocess.run(["bash", os.path.join(ROOT, "tools", "asan_build.sh")], check=True)
+        except (OSError, subprocess.CalledProcessError) as e:
+            # test-only artefact: a toolchain without the clang ASan runtime must not fail the product
+            # build; tests/test_gpu_lifecycle.py fails on its own when the binary is missing
+            print(f"efes_amd.build: the ASan lifecycle test was not built ({e})", file=sys.stderr)
+            return None
     return exe
 
 

@@ -139,8 +139,9 @@ __device__ __forceinline__ void load_line(const uint8_t* src, uint32_t (&w)[kLin
 // from inline assembly so the compiler does not see an LDS write in flight: it would otherwise
 // wait for the DMA before every table lookup (the slot is only read after the explicit wait in
 // span_kernel).  The lgkmcnt wait orders the slot's previous reads before the overwrite; M0 is the
-// slot's LDS byte address (one wait state between writing M0 and the DMA; M0 is a reserved register
-// the compiler does not take as a clobber).
+// slot's LDS byte address (one wait state between writing M0 and the DMA).  LLVM reserves M0: a "m0"
+// clobber is not honoured (clang warns and emits the same code), so the contract that nothing else
+// in span_kernel keeps a value in M0 is checked on the compiled ISA by tests/test_span_isa.py.
 //   slot unit (16 B) u = 4*line + ((piece + line/4) mod 4)
 //   lane l of instruction k: unit 64k + l -> line 16k + l/4, piece ((l mod 4) - l/16) mod 4
 __device__ __forceinline__ uint32_t fetch_offset(uint32_t lane) {
@@ -156,7 +157,7 @@ __device__ __forceinline__ void fetch_row(const uint8_t* src, uint32_t slot) {  
         "s_waitcnt lgkmcnt(0)\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off nt"
         :
         : "v"(src + 1024 * k), "s"(slot + 1024u * k)
-        : "memory");  // (M0 has no other user in span_kernel: checked in the ISA)
+        : "memory");  // M0: no other user in span_kernel (tests/test_span_isa.py)
 }
 
 // Raw CRC (from a zero register) of one line: slicing-by-4 (the 4-byte form of crc32.go:157-161).
@@ -268,6 +269,7 @@ hipError_t launch_crc_span(const void* data, uint64_t length, uint32_t* crc, con
                             : (uint64_t)((16 - (reinterpret_cast<uintptr_t>(d) & 15)) & 15);
   const uint64_t m = length - head, nline = m / kSpanLine, rest = m % kSpanLine;
   const uint8_t* bulk = d + head;
+  clear_last_error();
   hipLaunchKernelGGL(span_prep_kernel, dim3(1), dim3(64), 0, s, d, (uint32_t)head, (uint32_t)rest,
                      bulk + nline * kSpanLine, xpow8n(m), crc, tabs);
   hipError_t e = hipGetLastError();
@@ -298,6 +300,7 @@ hipError_t launch_crc_span(const void* data, uint64_t length, uint32_t* crc, con
   for (uint64_t d = 1; d < groups; ++d) pw[d] = gf2_mulmod(zrow, pw[d - 1]);
   for (uint64_t w = 0; w < groups; ++w)
     a.op[w] = w < rtot ? gf2_mulmod(base, pw[(rtot - 1 - w) % groups]) : 0u;
+  clear_last_error();
   hipLaunchKernelGGL(span_kernel, dim3((uint32_t)groups), dim3(kSpanLanes), 0, s, a);
   return hipGetLastError();
 }

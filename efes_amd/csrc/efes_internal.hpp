@@ -144,6 +144,12 @@ inline int group_of_mode(int mode) {
 
 constexpr int kDeepWaves = 4;  // waves per DEEP workgroup: one per SIMD
 
+// HIP keeps a failed call's error as the calling thread's last error until it is read, so a launcher
+// that reports hipGetLastError() after its launch clears it first: an earlier failure on the same
+// thread that was handled (a pinned allocation retried at half size, a LDS attribute that could not be
+// raised) must not come back as this launch's error.
+inline void clear_last_error() { (void)hipGetLastError(); }
+
 // Makes `dev` current for the scope and restores the caller's device (C ABI calls may come
 // from any host thread, efes_hash.h).
 struct DeviceGuard {
@@ -187,8 +193,7 @@ namespace efes {
 // streams: HIP spreads ALL of a process's streams over GPU_MAX_HW_QUEUES (4) queues, so two
 // ordinary streams may share one and serialize.  A stream created with a CU mask gets a queue of
 // its own (the mask is a queue property); the mask is every CU, so placement is unchanged.
-// EFES_PART_STREAMS=plain makes ordinary streams (A/B).  Used for the planned batch's part
-// streams and efes_hash_host's copy stream.  HIP creates CU-masked streams as blocking streams
+// Used for the planned batch's part streams and efes_hash_host's copy stream.  HIP creates CU-masked streams as blocking streams
 // (hipStreamDefault): they also order against the legacy NULL stream, which adds ordering,
 // never removes it.
 hipError_t own_queue_stream(const efes_ctx* ctx, hipStream_t* out);

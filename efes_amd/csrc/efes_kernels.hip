@@ -1528,6 +1528,7 @@ __global__ void fill_kernel(uint64_t* __restrict__ dst, uint64_t nwords, uint64_
 hipError_t launch_deep(const efes_job* jobs, uint32_t njobs, const Tables* tabs, hipStream_t s) {
   if (njobs == 0) return hipSuccess;
   const uint32_t grid = (njobs + kPipeJobs - 1) / kPipeJobs;
+  clear_last_error();
   hipLaunchKernelGGL(deep_kernel, dim3(grid), dim3(128 * kPipeJobs), 0, s, jobs, njobs, tabs);
   return hipGetLastError();
 }
@@ -1548,6 +1549,7 @@ hipError_t launch_reserving(K kernel, dim3 grid, dim3 block, bool exclusive, hip
         dyn = 0;  // cannot reserve: run shared
     }
   }
+  clear_last_error();
   hipLaunchKernelGGL(kernel, grid, block, dyn, s, jobs, njobs, tabs, more...);
   return hipGetLastError();
 }
@@ -1619,6 +1621,7 @@ hipError_t launch_wide(const efes_job* jobs, uint32_t njobs, const Tables* tabs,
   if (!big_ok && sizeof(WideLDS) + xs > 64 * 1024) return hipErrorInvalidConfiguration;
   // exclusive: reserve the CU's whole LDS, so no other workgroup shares its SIMDs
   const size_t dyn = exclusive && big_ok ? kCuLds - static_lds : xs;
+  clear_last_error();
   hipLaunchKernelGGL(wide_kernel, dim3((njobs + per - 1) / per), dim3(per), dyn, s, jobs, njobs, tabs);
   return hipGetLastError();
 }
@@ -1629,6 +1632,7 @@ hipError_t launch_fill(void* dst, size_t bytes, uint64_t seed, hipStream_t s) {
   uint64_t blocks = (nwords + 255) / 256;
   if (blocks > 8192) blocks = 8192;
   if (blocks == 0) blocks = 1;
+  clear_last_error();
   hipLaunchKernelGGL(fill_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, reinterpret_cast<uint64_t*>(dst), nwords,
                      seed, reinterpret_cast<uint8_t*>(dst) + nwords * 8, tail);
   return hipGetLastError();

@@ -408,6 +408,7 @@ int efes::queue_create_reclaiming(efes_ctx* ctx, uint64_t chunk_bytes, uint32_t 
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&q->stream, hipStreamNonBlocking);
   if (e != hipSuccess) {
     efes_queue_destroy(q);
+    efes::clear_last_error();  // the caller may retry smaller (create_digest_queue): not a later launch's error
     return EFES_ERR_HIP;
   }
   for (uint32_t i = max_chunks; i-- > 0;) q->free_chunks.push_back(i);

@@ -515,25 +515,46 @@ struct Call {
 };
 
 // The digest queue's reclaim hook (run by its dispatcher thread, which holds no digest, pair or
-// queue lock): every chunk sits partly filled in an upload while `want` writers wait for one, so
-// holders that are not inside a call hand their partly filled chunks over (hashed like a full one,
-// then freed), oldest first, until `want` chunks are on their way.  One holder is locked at a time
-// (a locked holder cannot be freed, parked or settled meanwhile) and the scan stops there, so an
-// idle digest's next call waits for one hand-over at most, not for a walk over every open upload.
-// (A fused pair's unconfirmed leader Write waits in its scratch buffer, never in the chunk.)
-// Lock order: dreg.mu, then a holder by try_lock, then the queue's mutex inside the hand-over --
-// nothing takes dreg.mu while holding a queue's mutex.  Returns whether anything was handed over.
+// queue lock): every chunk sits partly filled in an upload while `want` writers wait for one, so up
+// to `want` holders that are not inside a call hand their partly filled chunks over (hashed like a
+// full one, then freed).  Holders idle for kReclaimIdleNs or longer go first -- an abandoned or
+// stalled upload's chunk before that of one whose writer is between two Writes (which would fill it
+// soon anyway) -- then the other holders, oldest first.  They are try-locked under dreg.mu and handed
+// over after it is released (a locked holder cannot be freed, parked or settled meanwhile, as in
+// evict_one), so the context's acquire / adopt / evict calls never wait behind the hand-overs
+// (ADVICE r05).  (A fused pair's unconfirmed leader Write waits in its scratch buffer, never in the
+// chunk.)  Lock order: dreg.mu, then holders by try_lock only; the queue's mutex inside the hand-over
+// is taken with dreg.mu released -- nothing takes dreg.mu while holding a queue's mutex.  Returns
+// whether anything was handed over.
+constexpr int64_t kReclaimIdleNs = 1000000;  // 1 ms: longer than any gap between a writer's Writes
+
 bool reclaim_chunks(void* arg, uint32_t want) {
   efes_ctx* ctx = static_cast<efes_ctx*>(arg);
+  std::vector<std::pair<std::mutex*, efes_upload*>> held;
+  held.reserve(std::min<uint32_t>(want, 4096));
+  {
+    std::lock_guard<std::mutex> lk(ctx->dreg.mu);
+    const int64_t horizon = now_ns() - kReclaimIdleNs;
+    for (int pass = 0; pass < 2 && held.size() < want; ++pass) {
+      for (const OpenRef& r : ctx->dreg.open) {
+        if (held.size() >= want) break;
+        const bool idle = (r.d ? r.d->last_ns : r.f->last_ns).load(std::memory_order_relaxed) <= horizon;
+        if (idle != (pass == 0)) continue;  // pass 0: the idle holders; pass 1: the others
+        std::mutex& m = r.d ? r.d->mu : r.f->mu;
+        if (!m.try_lock()) continue;
+        efes_upload* u = r.d ? r.d->u : r.f->u;
+        if (u) {
+          held.emplace_back(&m, u);
+        } else {
+          m.unlock();
+        }
+      }
+    }
+  }
   uint32_t got = 0;
-  std::lock_guard<std::mutex> lk(ctx->dreg.mu);
-  for (const OpenRef& r : ctx->dreg.open) {
-    if (got >= want) break;
-    std::mutex& m = r.d ? r.d->mu : r.f->mu;
-    if (!m.try_lock()) continue;
-    efes_upload* u = r.d ? r.d->u : r.f->u;
-    if (u && efes::upload_handover(u)) ++got;
-    m.unlock();
+  for (auto& [m, u] : held) {
+    if (efes::upload_handover(u)) ++got;
+    m->unlock();
   }
   return got > 0;
 }

@@ -352,3 +352,57 @@ def test_evict_patience(gpu, patience_ms):
         assert waited < 0.5, waited
     else:
         assert 1.3 < waited < 10, waited
+
+
+_STALE_ERROR_CHILD = r"""
+import ctypes, hashlib, sys, zlib
+sys.path[:0] = [{root!r}]
+import torch
+from efes_amd import MODE_DEEP, hashing
+from efes_amd.batch import DeviceBatch
+hip = ctypes.CDLL("libamdhip64.so.7")  # the runtime torch loaded (one HIP runtime per process)
+hip.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
+
+def poison():
+    # a handled failure on this thread: HIP keeps it as the thread's last error until it is read
+    p = ctypes.c_void_p()
+    rc = hip.hipMalloc(ctypes.byref(p), 1 << 60)
+    assert rc != 0 and hip.hipPeekAtLastError() == rc, rc
+
+ctx = hashing.Context(0)
+s = torch.cuda.Stream()
+n = (8 << 20) + 3
+with torch.cuda.stream(s):
+    data = torch.empty(n, dtype=torch.uint8, device="cuda:0")
+    ctx.fill_synthetic(data.data_ptr(), n, 77, s.cuda_stream)
+    st = torch.zeros(1, dtype=torch.int64, device="cuda:0")
+    b = DeviceBatch(data.data_ptr(), [0, 1, 4096], [n - 1, 65, 1 << 20], ctx=ctx)
+s.synchronize()
+host = data.cpu().numpy().tobytes()
+poison()
+ctx.crc32_span(data.data_ptr() + 1, n - 1, st.data_ptr(), s.cuda_stream)  # raised EFES_ERR_HIP before the fix
+poison()
+rc = hashing.lib().efes_hash_submit_mode(ctx.handle, b.jobs.data_ptr(), b.n, s.cuda_stream, MODE_DEEP)
+assert rc == 0, rc
+s.synchronize()
+assert int(st.item()) & 0xFFFFFFFF == zlib.crc32(host[1:])
+want = [hashlib.sha1(host[o:o + k]).hexdigest() for o, k in ((0, n - 1), (1, 65), (4096, 1 << 20))]
+assert (b.status_host() == 0).all() and b.sha1_hex() == want, (b.status_host(), b.sha1_hex(), want)
+print("stale error ignored")
+"""
+
+
+def test_launches_ignore_a_stale_hip_error(gpu):
+    """HIP keeps a failed call as the thread's last error until it is read.  A handled
+    failure on the caller's thread -- here a hipMalloc too large to succeed; in the library, a pinned
+    staging allocation retried at half size -- must not come back as the error of the next span CRC or
+    job launch on that thread (every launcher clears the last error before it launches).  In a child
+    process, so the poisoned thread state cannot leak into torch's own launch checks."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", _STALE_ERROR_CHILD.format(root=root)], capture_output=True, text=True,
+                       timeout=110)
+    assert r.returncode == 0 and "stale error ignored" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])

@@ -875,6 +875,51 @@ def sha1_only_leg(args, ctx, data, fused, device: str, stream):
             "digests_match_fused_sha1": ok, "note": "same chunks as the metric, SHA-1 only; not `value`"}
 
 
+def device_bdf(dev_index: int):
+    """The PCI address of HIP device `dev_index` ("0000:05:00.0"; the clock probe's
+    hipDeviceGetPCIBusId, else torch's device properties), or None."""
+    import ctypes
+
+    path = os.path.join(ROOT, "tools", "libclockprobe.so")
+    if os.path.exists(path):
+        try:
+            buf = ctypes.create_string_buffer(64)
+            if ctypes.CDLL(path).clockprobe_pci_bus_id(dev_index, buf, 64) == 0 and buf.value:
+                return buf.value.decode().lower()
+        except (OSError, AttributeError):
+            pass
+    try:
+        import torch
+
+        p = torch.cuda.get_device_properties(dev_index)
+        return f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+    except Exception:  # noqa: BLE001
+        return None
+
+
+def rank_spot_check(args, data, batches, config) -> bool:
+    """hashlib/zlib of the first and last job of this rank's (first) batch against its Sums: the
+    headline's chunks and the mixed sizes directly, the segmented ingest through ingest_spot_check."""
+    import hashlib
+    import zlib
+
+    if config.get("segment_bytes"):
+        return ingest_spot_check(data, batches, config)
+    b = batches[0]
+    if not b.n:
+        return True
+    ok = bool((b.status_host() == 0).all())
+    sums = b.sums_host()
+    base = data.data_ptr()
+    for j in sorted({0, b.n - 1}):
+        off, n = int(b.jobs_host["data"][j]) - base, int(b.jobs_host["length"][j])
+        piece = data[off:off + n].cpu().numpy().tobytes()
+        ok = ok and bytes(sums[j][:20]) == hashlib.sha1(piece).digest()
+        if not args.sha1_only:
+            ok = ok and int.from_bytes(bytes(sums[j][20:24]), "big") == zlib.crc32(piece)
+    return bool(ok)
+
+
 def ingest_spot_check(data, batches, config) -> bool:
     """hashlib/zlib of two chunks per launch group against the Sums of the segmented ingest (chunk j
     of a group = its segment's bytes, once per segment); True when the leg is not segmented."""
@@ -1110,6 +1155,7 @@ def main(argv=None):
         steps = args.steps if len(batches) == 1 else len(batches)
         wall, kernel_ms, clock = run_timed(batches, steps, args.warmup, mode, device, stream, dist, args.progress)
     print(f"[bench] headline: {steps} steps in {wall:.3f} s on this rank", file=sys.stderr, flush=True)
+    rank_wall = wall
     wall = max_over_ranks(wall, device if args.dist_backend == "nccl" else None)  # slowest rank
 
     bytes_timed = sum(step_bytes[k % len(step_bytes)] for k in range(steps))
@@ -1161,6 +1207,18 @@ def main(argv=None):
     }
     if plan:
         out["config"]["plan"] = plan
+    # Which device each rank ran on, its own rate and kernel time, and spot checks of its digests
+    # (SURVEY.md §8(e)): a weak-scaling line must show N distinct GPUs doing the work.  After the timed
+    # region; one all_gather_object of a small dict, measurement only.
+    from efes_amd.shard import gather_rank_records, summarize_ranks
+
+    rec = {"rank": rank, "local_rank": local, "device": dev_index, "bdf": device_bdf(dev_index),
+           "GiB/s": round(bytes_timed / rank_wall / GiB, 3), "wall_s": round(rank_wall, 4),
+           "kernel_ms": round(kernel_ms, 4), "clock_mhz": clock.get("mhz"),
+           "spot_check": rank_spot_check(args, data, batches, config)}
+    records = gather_rank_records(rec)
+    out["ranks"] = records
+    out["ranks_check"] = summarize_ranks(records, world, args.all_ranks_on_device0)
     if args.workload == "chunks4m":
         n, chunk = args.chunks, args.chunk_bytes
         if args.host_inclusive == "on" or (args.host_inclusive == "auto" and world == 1):
@@ -1199,6 +1257,10 @@ def main(argv=None):
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
+    if not out["ranks_check"]["ok"]:
+        # after the line is out: the driver keeps the measurement, and the run still fails loudly
+        print(f"bench.py: rank check failed: {out['ranks_check']}", file=sys.stderr, flush=True)
+        sys.exit(3)
 
 
 if __name__ == "__main__":

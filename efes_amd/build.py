@@ -66,14 +66,15 @@ def build_tools() -> list[str]:
     out = []
     src = os.path.join(ROOT, "tools", "bench_uploads.cpp")
     exe = os.path.join(ROOT, "tools", "bench_uploads")
-    if os.path.exists(src) and _stale(exe, [src, LIB]):
+    devices_hpp = os.path.join(ROOT, "tools", "efes_devices.hpp")
+    if os.path.exists(src) and _stale(exe, [src, LIB, devices_hpp]):
         subprocess.run([hipcc(), "-O2", "-std=c++17", "-I", os.path.join(ROOT, "include"), src, "-o", exe,
                         "-L", LIB_DIR, "-lefeshash", "-Wl,-rpath,$ORIGIN/../efes_amd/lib", "-pthread"], check=True)
     if os.path.exists(exe):
         out.append(exe)
     src = os.path.join(ROOT, "tools", "bench_go_surface.cpp")
     exe = os.path.join(ROOT, "tools", "bench_go_surface")
-    if os.path.exists(src) and _stale(exe, [src, LIB, os.path.join(ROOT, "include", "efes_hash.h")]):
+    if os.path.exists(src) and _stale(exe, [src, LIB, os.path.join(ROOT, "include", "efes_hash.h"), devices_hpp]):
         subprocess.run(["g++", "-O2", "-std=c++17", "-Wall", "-Wextra", "-pthread", "-I", os.path.join(ROOT, "include"),
                         src, "-o", exe, "-L", LIB_DIR, "-lefeshash", "-Wl,-rpath,$ORIGIN/../efes_amd/lib"], check=True)
     if os.path.exists(exe):

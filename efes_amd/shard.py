@@ -121,3 +121,41 @@ def gather_piece_crcs(crc: int, length: int, device=None) -> list[tuple[int, int
     parts = [torch.empty_like(mine) for _ in range(dist.get_world_size())]
     dist.all_gather(parts, mine)
     return [(int(p[0].item()), int(p[1].item())) for p in parts]
+
+
+# ---- per-rank records of a multi-GPU bench (bench.py) -------------------------------
+# A weak-scaling line is only evidence of N GPUs if it shows that N distinct devices did the work:
+# every rank reports its device's PCI address, its own rate, its kernel time and spot checks of its
+# digests, and rank 0 checks that the addresses are distinct.
+
+
+def gather_rank_records(record: dict) -> list[dict]:
+    """Every rank's record, in rank order (all_gather_object; measurement only, after the timed region)."""
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return [dict(record)]
+    parts: list = [None] * dist.get_world_size()
+    dist.all_gather_object(parts, dict(record))
+    return parts
+
+
+def summarize_ranks(records: list[dict], world: int, rehearsal: bool = False) -> dict:
+    """The checks rank 0 makes on the gathered records: one record per rank, in order; the devices'
+    PCI addresses distinct (unless `rehearsal`: every rank on device 0 of a one-GPU box); every rank's
+    spot checks true.  `ok` is the conjunction; the rates are summed for comparison with `value`."""
+    ranks = [r.get("rank") for r in records]
+    bdfs = [r.get("bdf") for r in records]
+    known = [b for b in bdfs if b]
+    distinct = len(set(known)) == len(known) == world
+    out = {
+        "world": world,
+        "ranks_in_order": ranks == list(range(world)),
+        "distinct_devices": len(set(known)),
+        "devices_distinct": distinct,
+        "rehearsal_one_device": bool(rehearsal),
+        "spot_checks_ok": all(bool(r.get("spot_check")) for r in records),
+        "sum_rank_GiB/s": round(sum(float(r.get("GiB/s", 0.0)) for r in records), 3),
+    }
+    out["ok"] = out["ranks_in_order"] and out["spot_checks_ok"] and (distinct or bool(rehearsal))
+    return out

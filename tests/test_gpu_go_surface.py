@@ -64,3 +64,50 @@ def test_go_surface_harness_against_oracle(tmp_path, oracle, writes):
         assert res["pairs"] == uploads * patches and res["settles"] == 0, res
     else:
         assert res["hashed_bytes_per_byte"] == 2.0 and res["pairs"] == 0, res
+
+
+def test_go_surface_harness_over_a_pool_of_contexts():
+    """the Go-surface harness opens its contexts as hash_gpu.go's pool() does --
+    every visible GPU by default, here the ordinal list "0,0" (two contexts of GPU 0 stand in for two
+    GPUs of one server process) -- and reports per-device launches, jobs and bytes.  Both contexts
+    hash, their bytes add up to the run's, and every Sum equals hashlib/zlib."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    if not os.path.exists(EXE):
+        pytest.fail(f"{EXE} not built (__graft_entry__.build())")
+    size, write, threads, uploads, k = 1 << 20, 32 << 10, 8, 256, 8
+    r = subprocess.run([EXE, str(threads), str(uploads), str(size), str(write), str(k), "1", "256", "512", "-", "same",
+                        "0,0"], capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stdout + r.stderr
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    data = _xorshift(size)
+    assert res["errors"] == 0 and res["all_equal"], res
+    assert res["sum_sha1_crc32"] == hashlib.sha1(data).hexdigest() + "%08x" % zlib.crc32(data)
+    assert res["devices_opened"] == 2 and res["devices_skipped"] == 0 and res["staging_mib_per_gpu"] == 256, res
+    devs = res["devices"]
+    assert [d["ordinal"] for d in devs] == [0, 0] and all(d["jobs"] > 0 and d["bytes"] > 0 for d in devs), devs
+    assert sum(d["bytes"] for d in devs) == res["hashed_bytes_per_byte"] * uploads * size, devs
+
+
+def test_uploads_harness_over_queues_of_two_contexts():
+    """The uploads harness (bench.py's uploads_path) opens one efes_queue per device that opens and
+    places each upload on the queue with the most free slots (go/upload_gpu.go uploadQueue()); with
+    the ordinals "0,0" both queues hash, and every Sum equals hashlib/zlib."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    exe = os.path.join(ROOT, "tools", "bench_uploads")
+    if not os.path.exists(exe):
+        pytest.fail(f"{exe} not built (__graft_entry__.build())")
+    size = 1 << 20
+    r = subprocess.run([exe, "8", "256", str(size), str(32 << 10), "8", str(256 << 10), "0", "0,0"], capture_output=True,
+                       text=True, timeout=110)
+    assert r.returncode == 0, r.stdout + r.stderr
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    data = _xorshift(size)
+    assert res["errors"] == 0 and res["all_sums_equal"], res
+    assert res["sum_sha1_crc32"] == hashlib.sha1(data).hexdigest() + "%08x" % zlib.crc32(data)
+    devs = res["devices"]
+    assert res["devices_opened"] == 2 and [d["ordinal"] for d in devs] == [0, 0], res
+    assert all(d["jobs"] > 0 for d in devs) and sum(d["bytes"] for d in devs) == 256 * size, devs

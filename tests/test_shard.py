@@ -144,3 +144,57 @@ def test_two_rank_gloo_object_crc_matches_single_pass():
         assert p.exitcode == 0
     data = np.random.default_rng(21).integers(0, 256, 3_000_017, dtype=np.uint8).tobytes()
     assert got == {0: zlib.crc32(data), 1: zlib.crc32(data)}
+
+
+def _rank_worker(rank, world, port, q, same_device):
+    import torch.distributed as dist
+    from efes_amd.shard import gather_rank_records, summarize_ranks
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        bdf = "0000:05:00.0" if same_device else f"0000:{0x05 + 0x10 * rank:02x}:00.0"
+        rec = {"rank": rank, "local_rank": rank, "device": 0 if same_device else rank, "bdf": bdf,
+               "GiB/s": 86.0 + rank, "kernel_ms": 46.2, "wall_s": 0.93, "spot_check": True}
+        records = gather_rank_records(rec)
+        if rank == 0:
+            q.put((records, summarize_ranks(records, world), summarize_ranks(records, world, rehearsal=True)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("same_device", [False, True])
+def test_two_rank_gloo_rank_records(same_device):
+    """bench.py's N>1 line carries every rank's device (PCI address), rate, kernel
+    time and spot checks, gathered to rank 0, which checks that WORLD_SIZE distinct devices did the
+    work.  Two gloo ranks on CPU with stand-in records: distinct addresses pass; the same address on
+    both ranks fails the check unless the run is the one-GPU rehearsal (--all-ranks-on-device0)."""
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rank_worker, args=(r, 2, port, q, same_device)) for r in range(2)]
+    for p in procs:
+        p.start()
+    records, check, rehearsal = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [r["rank"] for r in records] == [0, 1] and [r["GiB/s"] for r in records] == [86.0, 87.0]
+    assert check["ranks_in_order"] and check["spot_checks_ok"] and check["sum_rank_GiB/s"] == 173.0
+    assert check["devices_distinct"] is (not same_device) and check["ok"] is (not same_device)
+    assert check["distinct_devices"] == (1 if same_device else 2)
+    assert rehearsal["ok"]  # the rehearsal runs every rank on device 0 on purpose
+
+
+def test_rank_summary_flags_bad_records():
+    from efes_amd.shard import summarize_ranks
+    good = [{"rank": r, "bdf": f"0000:0{r}:00.0", "GiB/s": 1.0, "spot_check": True} for r in range(4)]
+    assert summarize_ranks(good, 4)["ok"]
+    assert not summarize_ranks(good[:3], 4)["ok"]  # a rank missing
+    bad = [dict(r) for r in good]
+    bad[2]["spot_check"] = False
+    assert not summarize_ranks(bad, 4)["ok"]
+    unknown = [dict(r) for r in good]
+    unknown[1]["bdf"] = None  # an address that could not be read is not evidence of a distinct device
+    assert not summarize_ranks(unknown, 4)["devices_distinct"]

@@ -17,8 +17,13 @@
 // pair) or copy (the SHA-1 digest gets an equal copy at another address: the pair never binds, the
 // two digests are two uploads -- round 3's behaviour, each byte staged and hashed twice).
 // Not part of the product library.
+// Devices: like hash_gpu.go's pool(), one context per visible GPU (efes_device_count, a GPU whose
+// context fails is skipped) and one efes_pool over them -- a storage server is one process on every
+// GPU of its node (server.go:130) -- or the ordinals of `devices` ("0,0": two contexts of GPU 0).  The
+// staging per GPU is staging_mib / GPUs (at least 256 MiB); the line reports per-device launches,
+// jobs and bytes.
 //   tools/bench_go_surface <threads> <uploads> <upload_bytes> <write_bytes> [open_per_thread]
-//                          [patches] [chunk_kib] [staging_mib] [texts_out|-] [writes]
+//                          [patches] [chunk_kib] [staging_mib] [texts_out|-] [writes] [devices|all]
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -34,6 +39,7 @@
 
 #include "efes_hash.h"
 #include "cpu_quota.hpp"
+#include "efes_devices.hpp"
 
 namespace {
 
@@ -124,18 +130,23 @@ int main(int argc, char** argv) {
   const char* staging_mib = argc > 8 ? argv[8] : "8192";
   const char* texts_out = argc > 9 && strcmp(argv[9], "-") ? argv[9] : nullptr;
   const bool copy_writes = argc > 10 && !strcmp(argv[10], "copy");
+  const char* dev_list = argc > 11 ? argv[11] : "all";
   if (T < 1 || U < 1 || S < 1 || W < 1 || K < 1) return 2;
-  // The digest queue is created at the first digest Write: size it like bench_uploads' queue.
-  setenv("EFES_DIGEST_CHUNK_KIB", chunk_kib, 0);
-  setenv("EFES_DIGEST_STAGING_MIB", staging_mib, 0);
-  efes_ctx* ctx = nullptr;
-  int rc = efes_ctx_create(0, &ctx);
-  if (rc) {
-    fprintf(stderr, "efes_ctx_create: %s\n", efes_strerror(rc));
+  EfesDevices devs = efes_open_devices(dev_list);  // hash_gpu.go pool(): every GPU that opens
+  const int ndev = (int)devs.ctxs.size();
+  if (ndev == 0) {
+    fprintf(stderr, "no device opened (%d visible)\n", devs.visible);
     return 1;
   }
+  // The digest queues are created at each GPU's first digest Write: size them like bench_uploads'
+  // queue, the staging split over the GPUs.
+  char per_gpu_mib[32];
+  snprintf(per_gpu_mib, sizeof per_gpu_mib, "%ld", std::max(256L, atol(staging_mib) / ndev));
+  setenv("EFES_DIGEST_CHUNK_KIB", chunk_kib, 0);
+  setenv("EFES_DIGEST_STAGING_MIB", per_gpu_mib, 0);
+  int rc = 0;
   efes_pool* pool = nullptr;
-  rc = efes_pool_create(&ctx, 1, &pool);  // hash_gpu.go: one context per GPU, one pool
+  rc = efes_pool_create(devs.ctxs.data(), (uint32_t)ndev, &pool);  // hash_gpu.go: one context per GPU, one pool
   if (rc) {
     fprintf(stderr, "efes_pool_create: %s\n", efes_strerror(rc));
     return 1;
@@ -162,8 +173,22 @@ int main(int argc, char** argv) {
       return 1;
     }
   }
-  efes_queue_stats q0{};
-  efes_pool_stats(pool, 0, &q0);
+  auto pool_stats = [&] {
+    std::vector<efes_queue_stats> v(ndev);
+    for (int i = 0; i < ndev; ++i) efes_pool_stats(pool, (uint32_t)i, &v[i]);
+    return v;
+  };
+  auto total = [](const std::vector<efes_queue_stats>& v) {
+    efes_queue_stats t{};
+    for (const auto& x : v) {
+      t.launches += x.launches;
+      t.jobs += x.jobs;
+      t.bytes += x.bytes;
+    }
+    return t;
+  };
+  const std::vector<efes_queue_stats> d0 = pool_stats();
+  const efes_queue_stats q0 = total(d0);
   efes_pair_stats f0{};
   efes_pair_stats_get(&f0);
   std::mutex lat_mu;
@@ -192,8 +217,8 @@ int main(int argc, char** argv) {
     });
   for (auto& x : th) x.join();
   const double secs = std::chrono::duration<double>(clk::now() - t0).count();
-  efes_queue_stats q1{};
-  efes_pool_stats(pool, 0, &q1);
+  const std::vector<efes_queue_stats> d1 = pool_stats();
+  const efes_queue_stats q1 = total(d1);
   efes_pair_stats f1{};
   efes_pair_stats_get(&f1);
   if (texts_out) {  // for the oracle check in tests/test_gpu_go_surface.py
@@ -203,7 +228,8 @@ int main(int argc, char** argv) {
     }
   }
   efes_pool_destroy(pool);
-  efes_ctx_destroy(ctx);
+  const std::string per_dev = efes_devices_json(devs, d0, d1);
+  efes_close_devices(devs);
   char hex[49];
   for (int i = 0; i < 20; ++i) snprintf(hex + 2 * i, 3, "%02x", ex.sha[i]);
   for (int i = 0; i < 4; ++i) snprintf(hex + 40 + 2 * i, 3, "%02x", ex.crc[i]);
@@ -214,6 +240,8 @@ int main(int argc, char** argv) {
          "\"launches\": %llu, \"jobs\": %llu, \"hashed_bytes_per_byte\": %.4f, "
          "\"pairs\": %llu, \"fused_bytes_per_byte\": %.4f, \"settles\": %llu, "
          "\"patch_group_ms\": {\"p50\": %.3f, \"p90\": %.3f, \"p99\": %.3f, \"n\": %zu}, "
+         "\"devices_visible\": %d, \"devices_opened\": %d, \"devices_skipped\": %d, \"staging_mib_per_gpu\": %s, "
+         "\"devices\": %s, "
          "\"sum_sha1_crc32\": \"%s\", \"all_equal\": %s, \"errors\": %d}\n",
          pinned_cpus, T, U, S, W, K, P, chunk_kib, staging_mib,
          copy_writes ? "copy" : "same", secs,
@@ -221,6 +249,7 @@ int main(int argc, char** argv) {
          (unsigned long long)(q1.jobs - q0.jobs), (double)(q1.bytes - q0.bytes) / bytes,
          (unsigned long long)(f1.pairs - f0.pairs), (double)(f1.fused_bytes - f0.fused_bytes) / bytes,
          (unsigned long long)(f1.settles - f0.settles), pct(group_ms, 0.5), pct(group_ms, 0.9), pct(group_ms, 0.99),
-         group_ms.size(), hex, bad ? "false" : "true", errs.load());
+         group_ms.size(), devs.visible, ndev, devs.skipped, getenv("EFES_DIGEST_STAGING_MIB"), per_dev.c_str(), hex,
+         bad ? "false" : "true", errs.load());
   return errs || bad ? 1 : 0;
 }

@@ -1226,6 +1226,11 @@ def main(argv=None):
                                                    args.segment_bytes, batches[0])
         if not args.sha1_only and (args.sha1_leg == "on" or (args.sha1_leg == "auto" and world == 1)):
             out["sha1_only_config"] = legs.run("sha1_only_config", sha1_only_leg, args, ctx, data, batches[0], device, stream)
+        # the span CRC before the legs that allocate and free 64-200 GiB pools: its rate follows where its
+        # buffer lands (a 16 GiB buffer allocated after the mixed leg's 200 GiB pool read 5.8-6.0 TB/s
+        # where a fresh one read 6.6; DESIGN.md §4 "Span CRC"), and a standalone caller's buffer is fresh
+        if args.span_leg == "on" or (args.span_leg == "auto" and world == 1):
+            out["span_crc"] = legs.run("span_crc", span_crc_leg, args, ctx, device, stream)
         if args.ingest_leg in ("on", "auto"):
             out["ingest_config"] = legs.run("ingest_config", ingest_leg, args, rank, world, ctx, device, stream, MODE_AUTO,
                                             dist)
@@ -1245,8 +1250,6 @@ def main(argv=None):
             out["concurrency"] = legs.run("concurrency", concurrency_leg, args, ctx, device, stream)
         if args.mixed_leg == "on" or (args.mixed_leg == "auto" and world == 1):
             out["mixed_config"] = legs.run("mixed_config", mixed_leg, args, rank, world, ctx, device, stream)
-        if args.span_leg == "on" or (args.span_leg == "auto" and world == 1):
-            out["span_crc"] = legs.run("span_crc", span_crc_leg, args, ctx, device, stream)
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             threads = args.cpu_threads or host_threads()
             out["cpu_baseline"] = legs.run("cpu_baseline", cpu_baseline, batches[0], data, min(n, args.cpu_max_chunks), chunk,

@@ -103,6 +103,7 @@ _P, _S, _VP, _I, _U32, _U64 = ctypes.POINTER, ctypes.c_size_t, ctypes.c_void_p, 
 SIGNATURES = {
     "efes_strerror": (ctypes.c_char_p, [_I]),
     "efes_abi_version": (_I, []),
+    "efes_build_id": (ctypes.c_char_p, []),
     "efes_sha1_state_init": (None, [_P(Sha1State)]),
     "efes_device_count": (_I, []),
     "efes_ctx_create": (_I, [_I, _P(_VP)]),

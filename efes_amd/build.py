@@ -33,14 +33,33 @@ def _stale(target: str, deps: list[str]) -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+def _lib_deps() -> list[str]:
+    return ([os.path.join(CSRC, s) for s in SOURCES] + [os.path.join(CSRC, h) for h in HEADERS] +
+            [os.path.join(ROOT, "include", h) for h in PUBLIC_HEADERS])
+
+
+def source_id() -> str:
+    """The identity of the library's sources: the first 16 hex digits of a SHA-256 over every source and
+    header file (name and bytes, in a fixed order).  Compiled into the library (efes_build_id), so a
+    test on the GPU box can tell that the .so it loaded was built from the sources beside it."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for path in _lib_deps():
+        h.update(os.path.relpath(path, ROOT).encode() + b"\0")
+        with open(path, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
 def build_lib(force: bool = False, verbose: bool = False) -> str:
     srcs = [os.path.join(CSRC, s) for s in SOURCES]
-    deps = srcs + [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(ROOT, "include", h) for h in PUBLIC_HEADERS]
+    deps = _lib_deps()
     if not force and not _stale(LIB, deps):
         return LIB
     os.makedirs(LIB_DIR, exist_ok=True)
     tmp = LIB + ".tmp"
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", f'-DEFES_BUILD_ID="{source_id()}"',
            "-I", os.path.join(ROOT, "include"), "-o", tmp] + srcs
     if verbose:
         print(" ".join(cmd), file=sys.stderr)

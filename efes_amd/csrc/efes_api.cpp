@@ -147,6 +147,12 @@ hipError_t efes::own_queue_stream(const efes_ctx* ctx, hipStream_t* out) {
   return hipExtStreamCreateWithCUMask(out, (uint32_t)std::min(8, (ctx->cus + 31) / 32), all_cus);
 }
 
+// efes_amd/build.py passes -DEFES_BUILD_ID="<source_id()>"; other builds (A/B variants, sanitizer
+// builds) report that they were not built from a recorded source set.
+#ifndef EFES_BUILD_ID
+#define EFES_BUILD_ID "unversioned"
+#endif
+
 // ======================================================================= C ABI
 extern "C" {
 
@@ -165,6 +171,8 @@ const char* efes_strerror(int code) {
 }
 
 int efes_abi_version(void) { return EFES_ABI_VERSION; }
+
+const char* efes_build_id(void) { return EFES_BUILD_ID; }
 
 void efes_sha1_state_init(efes_sha1_state* s) {  // sha1.go:36-44 (x untouched, as Reset)
   s->h[0] = 0x67452301u; s->h[1] = 0xEFCDAB89u; s->h[2] = 0x98BADCFEu; s->h[3] = 0x10325476u; s->h[4] = 0xC3D2E1F0u;

@@ -47,6 +47,10 @@ extern "C" {
 
 const char* efes_strerror(int code);
 int efes_abi_version(void);
+/* The identity of the sources the library was built from (ABI 7): 16 hex digits of a SHA-256 over its
+ * source and header files, compiled in by efes_amd/build.py ("unversioned" for any other build), so a
+ * deployment -- and the GPU tests -- can check that the loaded library matches the sources beside it. */
+const char* efes_build_id(void);
 
 /* ---- state layouts (device- and host-side identical) ----------------------------- */
 

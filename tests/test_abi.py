@@ -414,7 +414,7 @@ def test_library_env_vars_are_the_documented_four():
     for f in os.listdir(os.path.join(ROOT, "efes_amd", "csrc")):
         src = open(os.path.join(ROOT, "efes_amd", "csrc", f)).read()
         names |= set(re.findall(r'getenv\("(\w+)"\)', src))
-        defines = set(re.findall(r"^#\s*if(?:n?def)?\s+(\w+)", src, flags=re.M)) - {"EFES_CHECKED"}
+        defines = set(re.findall(r"^#\s*if(?:n?def)?\s+(\w+)", src, flags=re.M)) - {"EFES_CHECKED", "EFES_BUILD_ID"}
         assert not {d for d in defines if d.startswith("EFES_")}, (f, defines)
     want = {"EFES_DIGEST_STAGING_MIB", "EFES_DIGEST_CHUNK_KIB", "EFES_DIGEST_SLOTS", "EFES_DIGEST_EVICT_MS"}
     assert names == want, names
@@ -504,3 +504,11 @@ def test_go_pool_opens_every_device_and_skips_failures():
     assert {"efes_gpu_devices_visible", "efes_gpu_devices_opened"} <= registered
     collect = next(body for r, t, n, body in _go_funcs(b) if n == "Collect")
     assert "len(gpuCtxs)" in collect and "gpuVisible" in collect and "strconv.Itoa(gpuDevs[i])" in collect
+
+
+def test_library_is_built_from_these_sources(efes_lib):
+    """efes_build_id() of the in-tree library == efes_amd.build.source_id() of the sources beside it
+    (a stale .so fails here, and the same check runs on the GPU box: tests/test_gpu_parity.py)."""
+    from efes_amd import build
+
+    assert efes_lib.lib().efes_build_id().decode() == build.source_id()

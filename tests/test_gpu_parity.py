@@ -1296,3 +1296,10 @@ def test_full_size_ingest_segmented_as_benched(env):
         assert ws[j] == hashlib.sha1(chunk).hexdigest() and int(wc[j]) == zlib.crc32(chunk), j
     del buf
     torch.cuda.empty_cache()
+
+
+def test_loaded_library_is_built_from_these_sources(env):
+    """The libefeshash.so this GPU process loaded was built from the sources in this tree (efes_build_id()
+    == efes_amd.build.source_id()): a stale prebuilt library shipped with the tree fails here."""
+    from efes_amd import _lib, build
+    assert _lib.lib().efes_build_id().decode() == build.source_id()

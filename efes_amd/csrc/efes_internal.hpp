@@ -84,6 +84,8 @@ int upload_confirm(efes_upload* u, const efes_sha1_state& shadow);
 // Hands u's partly filled current chunk to the dispatcher (the caller owns u: no call on it runs);
 // false when u holds none.
 bool upload_handover(efes_upload* u);
+// Whether u holds a partly filled chunk (the caller owns u, as for upload_handover).
+bool upload_partial(const efes_upload* u);
 
 // Streaming digests (efes_stream.cpp) that hold an upload of a context's digest queue, oldest
 // first: the candidates for eviction when a digest needs a state slot and none is free.  An

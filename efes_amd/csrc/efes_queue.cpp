@@ -723,6 +723,8 @@ int upload_confirm(efes_upload* u, const efes_sha1_state& shadow) {
   return u->latched;
 }
 
+bool upload_partial(const efes_upload* u) { return u->cur >= 0 && u->fill > 0; }
+
 bool upload_handover(efes_upload* u) {
   std::unique_lock<std::mutex> lk(u->q->mu);
   if (u->cur < 0 || u->fill == 0) return false;

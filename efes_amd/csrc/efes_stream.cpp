@@ -543,7 +543,7 @@ bool reclaim_chunks(void* arg, uint32_t want) {
         std::mutex& m = r.d ? r.d->mu : r.f->mu;
         if (!m.try_lock()) continue;
         efes_upload* u = r.d ? r.d->u : r.f->u;
-        if (u) {
+        if (u && efes::upload_partial(u)) {  // only holders that have a partly filled chunk to hand over
           held.emplace_back(&m, u);
         } else {
           m.unlock();

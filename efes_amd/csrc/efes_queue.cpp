@@ -69,10 +69,16 @@ struct Pending {
   uint64_t len;
 };
 
+using Clock = std::chrono::steady_clock;
+
 struct Batch {
   hipEvent_t ev = nullptr;
   std::vector<Pending> items;
   int jobs_half = 0;
+  int mode = 0;                // kernel shape it was launched with (efes::pcie_mode)
+  uint64_t max_len = 0;        // its longest job: the launch's time follows it
+  Clock::time_point start{};   // when it started running: its submit time on an idle stream, else the
+                               // retire time of the launch ahead of it (set then)
 };
 
 struct efes_queue {
@@ -110,18 +116,37 @@ struct efes_queue {
   // not keep a host core busy beside the request threads (receiver within noise either way:
   // profiles/r03_receiver/ab_sync_*.log).
   static constexpr unsigned ev_flags = hipEventDisableTiming | hipEventBlockingSync;
+  // Just-in-time assembly (round 6): while one launch runs, the next one is assembled only shortly
+  // before the running one is expected to end (DESIGN_NOTES.md §5 "One PATCH's latency under load"),
+  // so chunks staged meanwhile -- a new PATCH's first chunk above all -- still make that launch instead
+  // of waiting for the one after it.  The expected end comes from the launch's longest job and a
+  // learned time per byte of each kernel shape (EWMA over retired launches).
+  double ns_per_byte[16] = {};
   std::thread th;
 
   void run();
   void retire(Batch& b, std::unique_lock<std::mutex>& lk);
 };
 
+// Launches shorter than this are not timed for the per-byte model (launch overhead dominates them).
+constexpr uint64_t kJitMinBytes = 64u << 10;
+// How early the next launch is assembled before the running one's expected end: the host's wake-up,
+// the assembly, the job-array copy and the launch itself, plus the model's error.
+constexpr auto kJitMargin = std::chrono::microseconds(250);
+
 // Waits for the batch (without holding mu, so callers keep staging) and releases its chunks.
 void efes_queue::retire(Batch& b, std::unique_lock<std::mutex>& lk) {  // mu held on entry and exit
   lk.unlock();
   const bool ok = hipEventSynchronize(b.ev) == hipSuccess;
+  const Clock::time_point done = Clock::now();
   (void)hipEventDestroy(b.ev);
   lk.lock();
+  if (ok && b.max_len >= kJitMinBytes && b.mode >= 0 && b.mode < 16) {  // the launch time per byte of its shape
+    const double ns = std::chrono::duration<double, std::nano>(done - b.start).count() / (double)b.max_len;
+    double& r = ns_per_byte[b.mode];
+    r = r > 0 ? 0.75 * r + 0.25 * ns : ns;
+  }
+  if (!running.empty()) running.front().start = done;  // the launch queued behind it starts now
   if (!ok && fault == EFES_OK) fault = EFES_ERR_DEVICE_FAULT;
   for (const Pending& p : b.items) {
     if (p.slot != kNoChunk) free_chunks.push_back(p.slot);
@@ -167,6 +192,18 @@ void efes_queue::run() {
       running.pop_front();
       retire(b, lk);
       continue;
+    }
+    if (running.size() == 1 && !stop) {  // just in time: wait until shortly before it is expected to end
+      const Batch& r = running.front();
+      const double rate = r.mode >= 0 && r.mode < 16 ? ns_per_byte[r.mode] : 0.0;
+      if (rate > 0 && r.max_len >= kJitMinBytes) {
+        const auto end = r.start + std::chrono::nanoseconds((int64_t)(rate * (double)r.max_len));
+        const auto at = end - kJitMargin;
+        if (Clock::now() < at) {
+          work.wait_until(lk, at, [&] { return stop; });  // staging Writes do not cut the wait short
+          continue;
+        }
+      }
     }
     // Assemble: FIFO order, at most one chunk per upload (a job must not race its own state).
     Batch b;
@@ -223,9 +260,12 @@ void efes_queue::run() {
     if (e == hipSuccess) e = hipMemcpyAsync(dj, hj, sizeof(efes_job) * b.items.size(), hipMemcpyHostToDevice, stream);
     // DEEP (or grouped DEEP beyond one chunk per SIMD): efes::pcie_mode.
     const uint32_t nb = (uint32_t)b.items.size();
+    b.mode = efes::pcie_mode(ctx, nb);
+    for (const Pending& p : b.items) b.max_len = std::max<uint64_t>(b.max_len, p.len);
     int rc = e == hipSuccess ? EFES_OK : EFES_ERR_HIP;
     if (rc == EFES_OK && inject) rc = EFES_ERR_DEVICE_FAULT;  // as a faulted kernel
-    if (rc == EFES_OK) rc = efes_hash_submit_mode(ctx, dj, nb, stream, efes::pcie_mode(ctx, nb));
+    if (rc == EFES_OK) rc = efes_hash_submit_mode(ctx, dj, nb, stream, b.mode);
+    b.start = Clock::now();  // on an idle stream it starts now; else retire() sets it
     if (rc == EFES_OK && hipEventCreateWithFlags(&b.ev, ev_flags) != hipSuccess) rc = EFES_ERR_HIP;
     if (rc == EFES_OK && hipEventRecord(b.ev, stream) != hipSuccess) rc = EFES_ERR_HIP;
     lk.lock();

@@ -130,9 +130,10 @@ struct efes_queue {
 
 // Launches shorter than this are not timed for the per-byte model (launch overhead dominates them).
 constexpr uint64_t kJitMinBytes = 64u << 10;
-// How early the next launch is assembled before the running one's expected end: the host's wake-up,
-// the assembly, the job-array copy and the launch itself, plus the model's error.
-constexpr auto kJitMargin = std::chrono::microseconds(250);
+// How early the next launch is assembled before the running one's expected end: the host's wake-up
+// (late when the request threads keep every core of the quota busy), the assembly, the job-array copy
+// and the launch itself, plus the model's error -- 400 us plus a tenth of the expected time.
+constexpr auto kJitMargin = std::chrono::microseconds(400);
 
 // Waits for the batch (without holding mu, so callers keep staging) and releases its chunks.
 void efes_queue::retire(Batch& b, std::unique_lock<std::mutex>& lk) {  // mu held on entry and exit
@@ -193,12 +194,16 @@ void efes_queue::run() {
       retire(b, lk);
       continue;
     }
-    if (running.size() == 1 && !stop) {  // just in time: wait until shortly before it is expected to end
+    // Just in time: wait until shortly before the running launch is expected to end.  Only for DEEP
+    // launches (at most one job per SIMD: uploads in flight up to the SIMD count), whose time is one
+    // chunk's chain and barely varies; the grouped shapes of heavier loads launch ahead as before (there
+    // every upload has chunks waiting anyway, and a late wake-up would idle the GPU: profiles/r06_jit_ab/).
+    if (running.size() == 1 && !stop && running.front().mode == EFES_MODE_DEEP) {
       const Batch& r = running.front();
-      const double rate = r.mode >= 0 && r.mode < 16 ? ns_per_byte[r.mode] : 0.0;
+      const double rate = ns_per_byte[EFES_MODE_DEEP];
       if (rate > 0 && r.max_len >= kJitMinBytes) {
-        const auto end = r.start + std::chrono::nanoseconds((int64_t)(rate * (double)r.max_len));
-        const auto at = end - kJitMargin;
+        const auto dur = std::chrono::nanoseconds((int64_t)(rate * (double)r.max_len));
+        const auto at = r.start + dur - kJitMargin - dur / 10;
         if (Clock::now() < at) {
           work.wait_until(lk, at, [&] { return stop; });  // staging Writes do not cut the wait short
           continue;

@@ -512,3 +512,31 @@ def test_library_is_built_from_these_sources(efes_lib):
     from efes_amd import build
 
     assert efes_lib.lib().efes_build_id().decode() == build.source_id()
+
+
+def _go_code(src: str) -> str:
+    """src without comments and string literals (Go's lexical rules, enough for these files)."""
+    src = re.sub(r"/\*.*?\*/", " ", src, flags=re.S)
+    src = re.sub(r'"(?:\\.|[^"\\\n])*"|`[^`]*`', '""', src)
+    return re.sub(r"//[^\n]*", "", src)
+
+
+def test_go_files_import_exactly_what_they_use():
+    """No Go compiler here, so the compile errors that are cheap to see are checked as text: Go rejects
+    an unused import and a use of a package that is not imported, and every brace and parenthesis must
+    balance (go/*.go)."""
+    for name, src in _go_sources().items():
+        imports = re.search(r'^import \((.*?)^\)', src, flags=re.M | re.S).group(1)
+        pkgs = {}
+        for line in imports.splitlines():
+            m = re.match(r'\s*(\w+\s+)?"([\w./-]+)"', line)
+            if m:
+                pkgs[(m.group(1) or "").strip() or m.group(2).rsplit("/", 1)[-1]] = m.group(2)
+        code = _go_code(src.split(imports, 1)[1])
+        for alias in pkgs:
+            assert re.search(rf"(?<![\w.]){alias}\.", code), (name, "unused import", pkgs[alias])
+        std_used = set(re.findall(r"(?<![\w.])(errors|fmt|io|os|runtime|strconv|sync|atomic|unsafe|log|prometheus)\.\w", code))
+        assert std_used <= set(pkgs), (name, "not imported", std_used - set(pkgs))
+        whole = _go_code(src)
+        for a, b in ("{}", "()", "[]"):
+            assert whole.count(a) == whole.count(b), (name, a + b)

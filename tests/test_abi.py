@@ -429,7 +429,7 @@ def test_integration_load_rule_and_gauges():
     the ones the binding's collector registers; the collector never opens the GPUs itself."""
     doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
     rule = doc[doc.index("**Load rule for `efes-server`.**"):doc.index("## 2.")]
-    assert "patch_latency" in rule and "8.5 × C uploads are in flight" in rule
+    assert "patch_latency" in rule and "8 × C uploads are in flight" in rule
     binding = _binding()
     registered = set(re.findall(r'prometheus\.NewDesc\("(efes_gpu_\w+)"', binding))
     named = set(re.findall(r"`(efes_gpu_\w+)(?:\{gpu\})?`", rule))

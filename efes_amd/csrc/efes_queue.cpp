@@ -143,8 +143,12 @@ void efes_queue::retire(Batch& b, std::unique_lock<std::mutex>& lk) {  // mu hel
   (void)hipEventDestroy(b.ev);
   lk.lock();
   if (ok && b.max_len >= kJitMinBytes && b.mode >= 0 && b.mode < 16) {  // the launch time per byte of its shape
-    const double ns = std::chrono::duration<double, std::nano>(done - b.start).count() / (double)b.max_len;
+    // A sample is the launch's time plus this thread's wake-up, which the request threads can delay by
+    // milliseconds on a busy CPU quota: samples above 1.5 x the model are clipped there, so one late
+    // wake-up moves it by 12.5 % at most (the margin covers that) while real slowdowns still get in.
+    double ns = std::chrono::duration<double, std::nano>(done - b.start).count() / (double)b.max_len;
     double& r = ns_per_byte[b.mode];
+    if (r > 0) ns = std::min(ns, 1.5 * r);
     r = r > 0 ? 0.75 * r + 0.25 * ns : ns;
   }
   if (!running.empty()) running.front().start = done;  // the launch queued behind it starts now

@@ -141,13 +141,16 @@ def gather_rank_records(record: dict) -> list[dict]:
 
 
 def summarize_ranks(records: list[dict], world: int, rehearsal: bool = False) -> dict:
-    """The checks rank 0 makes on the gathered records: one record per rank, in order; the devices'
-    PCI addresses distinct (unless `rehearsal`: every rank on device 0 of a one-GPU box); every rank's
-    spot checks true.  `ok` is the conjunction; the rates are summed for comparison with `value`."""
+    """The checks rank 0 makes on the gathered records: one record per rank, in order; no two ranks on
+    one PCI address (unless `rehearsal`: every rank on device 0 of a one-GPU box; an address that could
+    not be read leaves `devices_distinct` None, which does not fail the run); every rank's spot checks
+    true.  `ok` is the conjunction; the rates are summed for comparison with `value`."""
     ranks = [r.get("rank") for r in records]
     bdfs = [r.get("bdf") for r in records]
     known = [b for b in bdfs if b]
-    distinct = len(set(known)) == len(known) == world
+    # True: every rank's address known and all different; False: two ranks on one address (positive
+    # evidence of a broken placement); None: an address could not be read, so the check cannot say
+    distinct = False if len(set(known)) < len(known) else (True if len(known) == world else None)
     out = {
         "world": world,
         "ranks_in_order": ranks == list(range(world)),
@@ -157,5 +160,5 @@ def summarize_ranks(records: list[dict], world: int, rehearsal: bool = False) ->
         "spot_checks_ok": all(bool(r.get("spot_check")) for r in records),
         "sum_rank_GiB/s": round(sum(float(r.get("GiB/s", 0.0)) for r in records), 3),
     }
-    out["ok"] = out["ranks_in_order"] and out["spot_checks_ok"] and (distinct or bool(rehearsal))
+    out["ok"] = out["ranks_in_order"] and out["spot_checks_ok"] and (distinct is not False or bool(rehearsal))
     return out

@@ -196,5 +196,8 @@ def test_rank_summary_flags_bad_records():
     bad[2]["spot_check"] = False
     assert not summarize_ranks(bad, 4)["ok"]
     unknown = [dict(r) for r in good]
-    unknown[1]["bdf"] = None  # an address that could not be read is not evidence of a distinct device
-    assert not summarize_ranks(unknown, 4)["devices_distinct"]
+    unknown[1]["bdf"] = None  # an address that could not be read: the check cannot say, and does not fail
+    assert summarize_ranks(unknown, 4)["devices_distinct"] is None and summarize_ranks(unknown, 4)["ok"]
+    dup = [dict(r) for r in unknown]
+    dup[3]["bdf"] = dup[0]["bdf"]  # two ranks on one device is positive evidence: fails
+    assert summarize_ranks(dup, 4)["devices_distinct"] is False and not summarize_ranks(dup, 4)["ok"]

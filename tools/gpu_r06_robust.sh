@@ -1,9 +1,8 @@
 #!/bin/bash
-# Round 6 robustness on the final library (the JIT dispatcher, the reclaim hand-over outside the registry lock): a long random fuzz of the fused digest pairs (3 000
-# scripts from 8 threads with the default 256 KiB staging chunks and 3 000 with 64 KiB chunks, seeds
-# beyond the test suite's, every text and digest against the oracle), (ThreadSanitizer: tools/gpu_r06_jit_ab3.sh).
-# digest layer whose reclaim hook and pair staging changed this round (build first:
-# bash tools/tsan_build.sh).
+# Round 6 robustness on the final library (the JIT dispatcher, the reclaim hand-over outside the
+# registry lock): a long random fuzz of the fused digest pairs (3 000 scripts from 8 threads with the
+# default 256 KiB staging chunks and 3 000 with 64 KiB chunks, seeds beyond the test suite's, every text
+# and digest against the oracle).  ThreadSanitizer over the same library: tools/gpu_r06_jit_ab3.sh.
 set -uo pipefail
 cd "${GRAFT_REPO_ROOT:?}" || exit 1
 O=gpurun_out/${1:-r06_robust}

@@ -1,8 +1,9 @@
 /*
  * efes_testing.h -- test hooks of libefeshash.so.  NOT part of the stable surface of efes_hash.h
- * (a binding such as INTEGRATION.md's hash_gpu.go never declares them): the symbols are exported so
+ * (a binding such as go/hash_gpu.go never declares them): the symbols are exported so
  * the library under test is the product build, and nothing reaches them except an explicit call --
- * no environment variable or configuration switches them on.
+ * no environment variable or configuration switches them on.  The risk of exporting them is stated in
+ * INTEGRATION.md §5.
  */
 #ifndef EFES_TESTING_H
 #define EFES_TESTING_H

@@ -79,6 +79,7 @@ struct Batch {
   uint64_t max_len = 0;        // its longest job: the launch's time follows it
   Clock::time_point start{};   // when it started running: its submit time on an idle stream, else the
                                // retire time of the launch ahead of it (set then)
+  bool start_known = false;    // submitted onto an idle stream: `start` is its submit time
 };
 
 struct efes_queue {
@@ -122,6 +123,12 @@ struct efes_queue {
   // of waiting for the one after it.  The expected end comes from the launch's longest job and a
   // learned time per byte of each kernel shape (EWMA over retired launches).
   double ns_per_byte[16] = {};
+  // Extra margin learned from gaps: when the launch a just-in-time wait was timed on had already
+  // finished by the time the next one was submitted (the dispatcher woke late: a busy CPU quota), the
+  // GPU idled; the margin then grows (x2 + 250 us, at most one launch) and shrinks by 1/8 per launch
+  // that was on time.
+  std::chrono::nanoseconds jit_extra{0};
+  bool jit_waited = false;  // the batch being assembled was timed by a just-in-time wait
   std::thread th;
 
   void run();
@@ -151,7 +158,7 @@ void efes_queue::retire(Batch& b, std::unique_lock<std::mutex>& lk) {  // mu hel
     if (r > 0) ns = std::min(ns, 1.5 * r);
     r = r > 0 ? 0.75 * r + 0.25 * ns : ns;
   }
-  if (!running.empty()) running.front().start = done;  // the launch queued behind it starts now
+  if (!running.empty() && !running.front().start_known) running.front().start = done;  // queued behind it: starts now
   if (!ok && fault == EFES_OK) fault = EFES_ERR_DEVICE_FAULT;
   for (const Pending& p : b.items) {
     if (p.slot != kNoChunk) free_chunks.push_back(p.slot);
@@ -207,8 +214,9 @@ void efes_queue::run() {
       const double rate = ns_per_byte[EFES_MODE_DEEP];
       if (rate > 0 && r.max_len >= kJitMinBytes) {
         const auto dur = std::chrono::nanoseconds((int64_t)(rate * (double)r.max_len));
-        const auto at = r.start + dur - kJitMargin - dur / 10;
+        const auto at = r.start + dur - kJitMargin - dur / 10 - jit_extra;
         if (Clock::now() < at) {
+          jit_waited = true;
           work.wait_until(lk, at, [&] { return stop; });  // staging Writes do not cut the wait short
           continue;
         }
@@ -261,7 +269,16 @@ void efes_queue::run() {
     }
     // test hook (efes_debug_fault_after): this launch reports a device fault instead of running
     const bool inject = inject_at && ++n_attempts == inject_at;
+    // the launch a just-in-time wait was timed on (the only one running): did it finish before this one?
+    const hipEvent_t timed_on = jit_waited && running.size() == 1 ? running.front().ev : nullptr;
+    const auto timed_dur = timed_on ? std::chrono::nanoseconds((int64_t)(ns_per_byte[EFES_MODE_DEEP] *
+                                                                         (double)running.front().max_len))
+                                    : std::chrono::nanoseconds(0);
+    jit_waited = false;
+    const bool idle_stream = running.empty();
     lk.unlock();  // callers keep staging while this batch is copied and launched
+    const bool late = timed_on && hipEventQuery(timed_on) == hipSuccess;  // already done: the GPU idles
+    if (timed_on) efes::clear_last_error();                                // (hipErrorNotReady: on time)
     // No H2D copy of the data: the DEEP kernel reads the pinned chunks in place (4 KiB per
     // wave per super-step, prefetched a super-step ahead, so the PCIe latency is hidden behind
     // the chain).  Measured 2.5x the rate of staging copies (DESIGN_NOTES.md).
@@ -275,9 +292,13 @@ void efes_queue::run() {
     if (rc == EFES_OK && inject) rc = EFES_ERR_DEVICE_FAULT;  // as a faulted kernel
     if (rc == EFES_OK) rc = efes_hash_submit_mode(ctx, dj, nb, stream, b.mode);
     b.start = Clock::now();  // on an idle stream it starts now; else retire() sets it
+    b.start_known = idle_stream || late;
     if (rc == EFES_OK && hipEventCreateWithFlags(&b.ev, ev_flags) != hipSuccess) rc = EFES_ERR_HIP;
     if (rc == EFES_OK && hipEventRecord(b.ev, stream) != hipSuccess) rc = EFES_ERR_HIP;
     lk.lock();
+    if (timed_on && rc == EFES_OK)
+      jit_extra = late ? std::min<std::chrono::nanoseconds>(2 * jit_extra + std::chrono::microseconds(250), timed_dur)
+                       : jit_extra - jit_extra / 8;
     if (rc != EFES_OK) {
       if (b.ev) (void)hipEventDestroy(b.ev);
       if (fault == EFES_OK) fault = rc;

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 6: just-in-time batch assembly in the upload dispatcher (efes_queue.cpp) against the previous
+# Round 6 (LIBS="product jitv3 prejit" for more builds): just-in-time batch assembly in the upload dispatcher (efes_queue.cpp) against the previous
 # dispatcher (tools/ab_variant.sh prejit "git:<rev>" efes_queue.cpp), interleaved on one box: one 4 MiB
 # PATCH's latency at 1 / 16 / 64 / 256 uploads in flight (the patch_latency leg's harness), the
 # unchanged Go surface at 8 192 in flight (go_surface_path) and efes_upload (uploads_path).  The
@@ -7,11 +7,15 @@
 set -uo pipefail
 cd "${GRAFT_REPO_ROOT:?}" || exit 1
 O=gpurun_out/${1:-r06_jit_ab}
-mkdir -p "$O" /tmp/ab_prejit
-cp efes_amd/lib/ab/libefeshash_prejit.so /tmp/ab_prejit/libefeshash.so
+LIBS=${LIBS:-product prejit}
+mkdir -p "$O"
+for lib in $LIBS; do
+  [ $lib = product ] && continue
+  mkdir -p /tmp/ab_$lib && cp efes_amd/lib/ab/libefeshash_$lib.so /tmp/ab_$lib/libefeshash.so
+done
 for rep in 1 2; do
-  for lib in product prejit; do
-    if [ $lib = product ]; then LP=""; else LP=/tmp/ab_prejit; fi
+  for lib in $LIBS; do
+    if [ $lib = product ]; then LP=""; else LP=/tmp/ab_$lib; fi
     for k in 1 16 64 256; do
       rounds=$([ $k = 1 ] && echo 20 || ([ $k -le 16 ] && echo 8 || ([ $k -le 64 ] && echo 6 || echo 4)))
       LD_LIBRARY_PATH=$LP timeout -k 10 120 ./tools/bench_go_surface $k $((k * rounds)) 4194304 32768 1 1 256 1024 \

@@ -129,13 +129,6 @@ struct efes_queue {
   // that was on time.
   std::chrono::nanoseconds jit_extra{0};
   bool jit_waited = false;  // the batch being assembled was timed by a just-in-time wait
-  Clock::time_point jit_at{};
-  // How late the dispatcher wakes from its just-in-time waits (EWMA, ns).  On a host whose cores are
-  // oversubscribed (hundreds of request threads on a 16-CPU quota) a timed wake-up can be milliseconds
-  // late and the GPU then idles with every upload in flight waiting (the PATCH tail at 192-256 in
-  // flight, DESIGN_NOTES.md §5); while the wake-ups run late the next launch is assembled ahead as
-  // before, and the average decays per launch so the timing is tried again later.
-  double jit_late_ns = 0;
   std::thread th;
 
   void run();
@@ -148,9 +141,6 @@ constexpr uint64_t kJitMinBytes = 64u << 10;
 // (late when the request threads keep every core of the quota busy), the assembly, the job-array copy
 // and the launch itself, plus the model's error -- 400 us plus a tenth of the expected time.
 constexpr auto kJitMargin = std::chrono::microseconds(400);
-// Average wake-up lateness above which the dispatcher stops timing launches (a timer wake-up of an
-// idle host is ~50-70 us late: the default timer slack).
-constexpr double kJitMaxLateNs = 200e3;
 
 // Waits for the batch (without holding mu, so callers keep staging) and releases its chunks.
 void efes_queue::retire(Batch& b, std::unique_lock<std::mutex>& lk) {  // mu held on entry and exit
@@ -219,25 +209,18 @@ void efes_queue::run() {
     // launches (at most one job per SIMD: uploads in flight up to the SIMD count), whose time is one
     // chunk's chain and barely varies; the grouped shapes of heavier loads launch ahead as before (there
     // every upload has chunks waiting anyway, and a late wake-up would idle the GPU: profiles/r06_jit_ab/).
-    if (running.size() == 1 && !stop && running.front().mode == EFES_MODE_DEEP && !jit_waited) {
+    if (running.size() == 1 && !stop && running.front().mode == EFES_MODE_DEEP) {
       const Batch& r = running.front();
       const double rate = ns_per_byte[EFES_MODE_DEEP];
-      if (jit_late_ns >= kJitMaxLateNs) {
-        jit_late_ns *= 0.9;  // waking late: launch ahead this time, try the timing again later
-      } else if (rate > 0 && r.max_len >= kJitMinBytes) {
+      if (rate > 0 && r.max_len >= kJitMinBytes) {
         const auto dur = std::chrono::nanoseconds((int64_t)(rate * (double)r.max_len));
         const auto at = r.start + dur - kJitMargin - dur / 10 - jit_extra;
         if (Clock::now() < at) {
           jit_waited = true;
-          jit_at = at;
           work.wait_until(lk, at, [&] { return stop; });  // staging Writes do not cut the wait short
           continue;
         }
       }
-    }
-    if (jit_waited) {  // woke from the wait: how late
-      const double late = std::chrono::duration<double, std::nano>(Clock::now() - jit_at).count();
-      jit_late_ns = 0.75 * jit_late_ns + 0.25 * std::max(0.0, late);
     }
     // Assemble: FIFO order, at most one chunk per upload (a job must not race its own state).
     Batch b;

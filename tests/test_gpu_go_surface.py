@@ -66,27 +66,30 @@ def test_go_surface_harness_against_oracle(tmp_path, oracle, writes):
         assert res["hashed_bytes_per_byte"] == 2.0 and res["pairs"] == 0, res
 
 
-def test_go_surface_harness_over_a_pool_of_contexts():
+@pytest.mark.parametrize("ncontexts", [2, 8])
+def test_go_surface_harness_over_a_pool_of_contexts(ncontexts):
     """the Go-surface harness opens its contexts as hash_gpu.go's pool() does --
-    every visible GPU by default, here the ordinal list "0,0" (two contexts of GPU 0 stand in for two
-    GPUs of one server process) -- and reports per-device launches, jobs and bytes.  Both contexts
-    hash, their bytes add up to the run's, and every Sum equals hashlib/zlib."""
+    every visible GPU by default, here the ordinal list "0,0" or eight times 0 (contexts of GPU 0 stand
+    in for the GPUs of one server process, up to an 8-GPU node's pool of eight digest queues) -- and
+    reports per-device launches, jobs and bytes.  Every context hashes, their bytes add up to the run's,
+    and every Sum equals hashlib/zlib."""
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     if not os.path.exists(EXE):
         pytest.fail(f"{EXE} not built (__graft_entry__.build())")
     size, write, threads, uploads, k = 1 << 20, 32 << 10, 8, 256, 8
-    r = subprocess.run([EXE, str(threads), str(uploads), str(size), str(write), str(k), "1", "256", "512", "-", "same",
-                        "0,0"], capture_output=True, text=True, timeout=110)
+    staging = 256 * ncontexts  # 256 MiB per context
+    r = subprocess.run([EXE, str(threads), str(uploads), str(size), str(write), str(k), "1", "256", str(staging), "-",
+                        "same", ",".join(["0"] * ncontexts)], capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stdout + r.stderr
     res = json.loads(r.stdout.strip().splitlines()[-1])
     data = _xorshift(size)
     assert res["errors"] == 0 and res["all_equal"], res
     assert res["sum_sha1_crc32"] == hashlib.sha1(data).hexdigest() + "%08x" % zlib.crc32(data)
-    assert res["devices_opened"] == 2 and res["devices_skipped"] == 0 and res["staging_mib_per_gpu"] == 256, res
+    assert res["devices_opened"] == ncontexts and res["devices_skipped"] == 0 and res["staging_mib_per_gpu"] == 256, res
     devs = res["devices"]
-    assert [d["ordinal"] for d in devs] == [0, 0] and all(d["jobs"] > 0 and d["bytes"] > 0 for d in devs), devs
+    assert [d["ordinal"] for d in devs] == [0] * ncontexts and all(d["jobs"] > 0 and d["bytes"] > 0 for d in devs), devs
     assert sum(d["bytes"] for d in devs) == res["hashed_bytes_per_byte"] * uploads * size, devs
 
 

@@ -540,3 +540,28 @@ def test_go_files_import_exactly_what_they_use():
         whole = _go_code(src)
         for a, b in ("{}", "()", "[]"):
             assert whole.count(a) == whole.count(b), (name, a + b)
+
+
+def test_go_files_use_only_declared_c_types_and_fields():
+    """Every C type the cgo files name (`C.efes_*`, `C.uint32_t`, ...) is declared by include/efes_hash.h or
+    is a standard C type, and every field they read from a C struct (`st.free_uploads`, `ps.settles`, ...)
+    is a member of that struct in the header -- compile errors cgo would report, checked as text."""
+    hdr = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    types = set(re.findall(r"typedef struct (\w+)", hdr)) | set(re.findall(r"}\s*(\w+);", hdr))
+    members = {}
+    for name, body in re.findall(r"typedef struct (\w+) \{(.*?)\}", hdr, flags=re.S):
+        members[name] = set(re.findall(r"(\w+)(?:\[\w*\])?;", body))
+    std = {"int", "char", "size_t", "uint8_t", "uint32_t", "uint64_t", "int32_t", "int64_t",
+           "GoString", "CString", "GoBytes"}  # cgo's own helpers
+    funcs = set(declared_functions())
+    for name, src in _go_sources().items():
+        code = _go_code(src)
+        used = set(re.findall(r"\bC\.(\w+)", code))
+        consts = {u for u in used if u.isupper() or u.startswith("EFES_")}
+        unknown = used - funcs - types - std - consts
+        assert not unknown, (name, unknown)
+        # fields read from stats structs: `var st C.efes_queue_stats` ... `st.field`
+        for var, ctype in re.findall(r"var (\w+) C\.(\w+)", code):
+            if ctype in members:
+                for field in set(re.findall(rf"\b{var}\.(\w+)", code)):
+                    assert field in members[ctype], (name, ctype, field)

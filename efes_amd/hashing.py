@@ -25,7 +25,7 @@ import numpy as np
 
 from ._lib import MODE_AUTO, EfesError, PairStats, Plan, QueueStats, Sha1State, check, lib
 
-__all__ = ["Context", "default_context", "crc32_combine", "Sha1Digest", "CRC32Digest", "Sha1File", "Digest", "FileInfo",
+__all__ = ["Context", "default_context", "device_count", "open_devices", "crc32_combine", "Sha1Digest", "CRC32Digest", "Sha1File", "Digest", "FileInfo",
            "new_sha1", "new_crc32_ieee", "EfesError"]
 
 
@@ -159,6 +159,28 @@ class Pool:
             now = self._live == 0
         if now:
             self._destroy()
+
+
+def device_count() -> int:
+    """efes_device_count (ABI 7): HIP devices the process sees, of any architecture (0 without any)."""
+    return int(lib().efes_device_count())
+
+
+def open_devices(devices=None) -> tuple[list[Context], list[tuple[int, str]]]:
+    """The contexts of go/hash_gpu.go's pool(): one per ordinal of `devices` (default: every ordinal
+    below device_count()), skipping -- never stopping at -- the ones whose efes_ctx_create fails.
+    Returns (contexts that opened, [(ordinal, reason) of each one skipped])."""
+    ctxs, skipped = [], []
+    for dev in (range(device_count()) if devices is None else devices):
+        try:
+            ctxs.append(Context(int(dev)))
+        except EfesError as e:
+            skipped.append((int(dev), strerror_of(e.code)))
+    return ctxs, skipped
+
+
+def strerror_of(code: int) -> str:
+    return lib().efes_strerror(code).decode()
 
 
 def pair_stats() -> dict:

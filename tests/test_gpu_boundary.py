@@ -12,6 +12,7 @@ with 65 536 (chunk reclaim by the dispatcher):
 and the multi-GPU pool (efes_pool_*): 16 request threads' digests spread over two contexts
 (standing in for two GPUs), both queues doing work, every text and Sum equal to the oracle's.
 """
+import gc
 import hashlib
 import json
 import random
@@ -406,3 +407,36 @@ def test_launches_ignore_a_stale_hip_error(gpu):
     r = subprocess.run([sys.executable, "-c", _STALE_ERROR_CHILD.format(root=root)], capture_output=True, text=True,
                        timeout=110)
     assert r.returncode == 0 and "stale error ignored" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])
+
+
+def test_python_open_devices_skips_a_failing_ordinal(gpu, oracle):
+    """The Python host layer's mirror of go/hash_gpu.go pool(): open_devices() opens every ordinal below
+    efes_device_count(), and with an explicit list it skips a failing ordinal in the middle and goes on;
+    a Pool over the contexts that opened hashes on all of them, every text equal to the oracle's."""
+    hashing = gpu["hashing"]
+    n = hashing.device_count()
+    assert n >= 1
+    every, skipped = hashing.open_devices()
+    assert [c.device for c in every] == list(range(n)) and skipped == []
+    for c in every:
+        c.close()
+    ctxs, skipped = hashing.open_devices([0, n, 0])
+    assert [c.device for c in ctxs] == [0, 0] and skipped == [(n, "invalid argument")]
+    pool = hashing.Pool(ctxs)
+    fis, fi = [], None
+    try:
+        for i in range(16):
+            body = _payload(100_000 + i, 900 + i)
+            fi = hashing.FileInfo(pool=pool)
+            _patch(hashing, fi, body)
+            fis.append((fi, body))
+        for fi, body in fis:
+            assert fi.digest.sha1.marshal_text().decode() == _oracle_text(oracle, body)
+            assert fi.digest.crc32.sum32() == zlib.crc32(body)
+        assert pool.stats(0).jobs > 0 and pool.stats(1).jobs > 0
+    finally:
+        fis = fi = None  # the digests go first (a pool outlives its digests, the contexts the pool)
+        gc.collect()
+        pool.close()
+        for c in ctxs:
+            c.close()
